@@ -1,0 +1,27 @@
+# Builds libgym_amd.so (gfx950 HIP kernels behind the C ABI in include/gym_amd.h)
+# in-tree, so the .so travels to the GPU box with the repo snapshot.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+SRC := $(wildcard gym_amd/csrc/*.hip)
+OBJ := $(patsubst gym_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB := gym_amd/_lib/libgym_amd.so
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -fvisibility=hidden -Wall -Wno-unused-function
+
+.PHONY: all clean oracle
+all: $(LIB)
+
+build/%.o: gym_amd/csrc/%.hip gym_amd/csrc/ga_common.h include/gym_amd.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	@mkdir -p gym_amd/_lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
+
+# ISA listing for inspection (register counts, MFMA/VALU mix).
+build/%.s: gym_amd/csrc/%.hip
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o $@
+
+clean:
+	rm -rf build $(LIB)

@@ -1,0 +1,368 @@
+// DeMo DCT codec on gfx950: chunked DCT-II encode + per-chunk top-k + residual
+// update (ga_demo_encode) and the gathered scatter-mean + inverse DCT + sign-SGD
+// apply (ga_demo_decode).  One 256-lane workgroup (4 waves) per chunk.
+//
+// Every transform is a pair of 64x64x64 fp32 products on the matrix cores
+// (v_mfma_f32_32x32x2_f32: exact f32 FMA chains in k order, each wave owns one
+// 32x32 quadrant of the product).  Chunks with n1, n2 < 64 are computed zero
+// padded: the 64x64 basis tables are zero outside n x n, so padded rows and
+// columns of every product are exactly 0 and never selected.
+//
+// LDS per workgroup: two 64x65 fp32 tiles (row stride 65 keeps the column reads
+// of the A operand conflict free) + a 256-bin histogram: ~34 KB.
+//
+// Top-k (demo.py:315-328, torch.topk(|x|, k, sorted=False)) is an exact radix
+// select on the |y| bit pattern (4 rounds of 8 bits) followed by an ordered
+// compaction; among coefficients tied with the k-th magnitude the lowest
+// coefficient index wins, and a chunk's entries are emitted in ascending index
+// order (the reference's order is unspecified; only the set matters).
+#include "ga_common.h"
+
+namespace ga {
+
+constexpr int kDmBlock = 256;
+constexpr int kLd = 65;
+constexpr int kTile = 64 * kLd;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Quadrant of C = opA . Bm (64x64x64) for this wave.
+//   A_ROW_LDS: A[i][k] = A[i*kLd + k] (LDS tile); else A[i][k] = A[k*64 + i] (a
+//   transposed 64x64 global table: the F1^T / B1^T of the left transform).
+//   B_LDS:     B[k][j] = Bm[k*kLd + j] (LDS tile); else Bm[k*64 + j] (global table).
+template <bool A_ROW_LDS, bool B_LDS>
+__device__ __forceinline__ f32x16 mm64(const float* A, const float* Bm) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = 32 * (w >> 1) + (lane & 31);
+    const int j = 32 * (w & 1) + (lane & 31);
+    const int h = lane >> 5;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+        const int k = 2 * s + h;
+        const float a = A_ROW_LDS ? A[i * kLd + k] : A[k * 64 + i];
+        const float b = B_LDS ? Bm[k * kLd + j] : Bm[k * 64 + j];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+// Row of accumulator register r for this lane (C/D layout of the 32x32 MFMA).
+__device__ __forceinline__ int acc_row(int r) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    return 32 * (w >> 1) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+__device__ __forceinline__ int acc_col() {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    return 32 * (w & 1) + (lane & 31);
+}
+
+__device__ __forceinline__ void store_acc(float* tile, const f32x16& acc) {
+    const int c = acc_col();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[acc_row(r) * kLd + c] = acc[r];
+}
+
+// Chunk -> tensor descriptor by a parallel scan of chunk_start (no serial
+// dependent loads): returns the descriptor index, identical in every lane.
+__device__ __forceinline__ int find_tensor(const ga_demo_tensor* T, int ntens, int chunk, int* slot) {
+    for (int t = threadIdx.x; t < ntens; t += kDmBlock) {
+        const int s0 = T[t].chunk_start;
+        const int s1 = (t + 1 < ntens) ? T[t + 1].chunk_start : 0x7fffffff;
+        if (s0 <= chunk && chunk < s1) *slot = t;
+    }
+    __syncthreads();
+    return *slot;
+}
+
+// Exclusive scan of one int per lane over the 256-lane workgroup.
+__device__ __forceinline__ int scan256(int v, int* wave_tot) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wave_tot[wid] = x;
+    __syncthreads();
+    int pre = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) pre += (w < wid) ? wave_tot[w] : 0;
+    __syncthreads();
+    return pre + x - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
+    const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ F,
+    const float* __restrict__ B, T* param, const T* __restrict__ grad, T* delta, int64_t ld, float lr,
+    float decay, float wd_factor, int32_t* payload, int64_t pstride, int64_t M) {
+    __shared__ float X[kTile];
+    __shared__ float Y[kTile];
+    __shared__ int hist[256];
+    __shared__ int misc[8];
+
+    const int chunk = blockIdx.x;
+    const int tix = find_tensor(tens, ntens, chunk, &misc[0]);
+    const ga_demo_tensor td = tens[tix];
+    const int c = chunk - td.chunk_start;
+    const int cy = c / td.gx, cx = c - cy * td.gx;
+    const int64_t rep = blockIdx.y;
+    param += rep * ld;
+    grad += rep * ld;
+    delta += rep * ld;
+    payload += rep * pstride;
+    const int64_t base = td.offset + (int64_t)cy * td.n1 * td.cols + (int64_t)cx * td.n2;
+    const int n1 = td.n1, n2 = td.n2;
+
+    // 1. error feedback: delta = decay*delta + lr*grad (and the decoupled weight decay)
+    for (int e = threadIdx.x; e < 4096; e += kDmBlock) {
+        const int h = e >> 6, w = e & 63;
+        float v = 0.f;
+        if (h < n1 && w < n2) {
+            const int64_t a = base + (int64_t)h * td.cols + w;
+            if (wd_factor != 1.f) Elem<T>::store(param + a, Elem<T>::load(param + a) * wd_factor);
+            float d = Elem<T>::load(delta + a);
+            if (decay != 1.f) d = d * decay;
+            v = fmaf(lr, Elem<T>::load(grad + a), d);
+        }
+        X[h * kLd + w] = v;
+    }
+    __syncthreads();
+
+    // 2. Y = F1^T . X . F2
+    f32x16 acc = mm64<true, false>(X, F + (int64_t)td.basis2 * 4096);
+    store_acc(Y, acc);
+    __syncthreads();
+    acc = mm64<false, true>(F + (int64_t)td.basis1 * 4096, Y);
+    __syncthreads();
+    store_acc(Y, acc);
+    __syncthreads();
+
+    // 3. top-k of |Y| over the valid n1 x n2 region; lane t owns coefficients
+    //    16t .. 16t+15 of the padded row-major 64x64 grid.
+    const int row = threadIdx.x >> 2, col0 = 16 * (threadIdx.x & 3);
+    uint32_t key[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const bool valid = row < n1 && (col0 + j) < n2;
+        key[j] = valid ? (__float_as_uint(Y[row * kLd + col0 + j]) & 0x7fffffffu) + 1u : 0u;
+    }
+    uint32_t prefix = 0, pmask = 0;
+    int kk = td.k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[threadIdx.x] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if ((key[j] & pmask) == prefix) atomicAdd(&hist[(key[j] >> shift) & 255u], 1);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            int hb[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) hb[b] = hist[4 * lane + b];
+            const int lsum = hb[0] + hb[1] + hb[2] + hb[3];
+            int x = lsum;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_down(x, d, 64);
+                if (lane + d < 64) x += y;
+            }
+            int cum = x - lsum;  // count in bins above this lane's bins
+#pragma unroll
+            for (int b = 3; b >= 0; --b) {
+                if (cum < kk && cum + hb[b] >= kk) {
+                    misc[1] = 4 * lane + b;
+                    misc[2] = kk - cum;
+                }
+                cum += hb[b];
+            }
+        }
+        __syncthreads();
+        prefix |= (uint32_t)misc[1] << shift;
+        pmask |= 0xffu << shift;
+        kk = misc[2];
+        __syncthreads();
+    }
+    // prefix == key of the k-th largest magnitude; take every larger key and
+    // the first kk keys equal to it in coefficient order.
+    int eq = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) eq += key[j] == prefix;
+    int eq_run = scan256(eq, &misc[4]);
+    uint32_t sel = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (key[j] > prefix) sel |= 1u << j;
+        else if (key[j] == prefix) {
+            if (eq_run < kk) sel |= 1u << j;
+            ++eq_run;
+        }
+    }
+    int slot = scan256(__popc(sel), &misc[4]);
+    int32_t* out_idx = payload + td.payload_off + (int64_t)c * td.k;
+    float* out_val = reinterpret_cast<float*>(payload + M) + td.payload_off + (int64_t)c * td.k;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        float& y = Y[row * kLd + col0 + j];
+        if (sel & (1u << j)) {
+            out_idx[slot] = row * n2 + col0 + j;
+            out_val[slot] = y;
+            ++slot;
+        } else {
+            y = 0.f;  // Y becomes the sparse S of the kept coefficients
+        }
+    }
+    __syncthreads();
+
+    // 4. delta -= B1^T . S . B2  (the estimate of what was transmitted)
+    acc = mm64<true, false>(Y, B + (int64_t)td.basis2 * 4096);
+    __syncthreads();
+    store_acc(Y, acc);
+    __syncthreads();
+    acc = mm64<false, true>(B + (int64_t)td.basis1 * 4096, Y);
+    const int cc = acc_col();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int rr = acc_row(r);
+        if (rr < n1 && cc < n2) {
+            const int64_t a = base + (int64_t)rr * td.cols + cc;
+            Elem<T>::store(delta + a, X[rr * kLd + cc] - acc[r]);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
+    const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ B,
+    const int32_t* __restrict__ payload, int64_t pstride, int64_t M, int64_t nsrc, T* param, T* grad,
+    int64_t K, int64_t ld, float lr) {
+    __shared__ float S[kTile];
+    __shared__ int cnt[4096];
+    __shared__ int misc[4];
+
+    const int chunk = blockIdx.x;
+    const int tix = find_tensor(tens, ntens, chunk, &misc[0]);
+    const ga_demo_tensor td = tens[tix];
+    const int c = chunk - td.chunk_start;
+    const int cy = c / td.gx, cx = c - cy * td.gx;
+    const int n1 = td.n1, n2 = td.n2, nk = td.k, nvalid = n1 * n2;
+    const int64_t base = td.offset + (int64_t)cy * n1 * td.cols + (int64_t)cx * n2;
+
+    for (int e = threadIdx.x; e < kTile; e += kDmBlock) S[e] = 0.f;
+    for (int e = threadIdx.x; e < 4096; e += kDmBlock) cnt[e] = 0;
+    __syncthreads();
+
+    // scatter-mean (demo.py:331-352): sources in node order; one source's
+    // indices are distinct, so each source is one conflict-free pass and the
+    // per-coefficient sums accumulate in node order.
+    const int64_t eoff = td.payload_off + (int64_t)c * nk;
+    for (int64_t s = 0; s < nsrc; ++s) {
+        const int32_t* pi = payload + s * pstride + eoff;
+        const float* pv = reinterpret_cast<const float*>(payload + s * pstride + M) + eoff;
+        for (int j = threadIdx.x; j < nk; j += kDmBlock) {
+            const int x = pi[j];
+            if (x >= 0 && x < nvalid) {
+                const int b = x / n2, d = x - b * n2;
+                S[b * kLd + d] += pv[j];
+                cnt[b * 64 + d] += 1;
+            }
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < 4096; e += kDmBlock) {
+        const int n = cnt[e];
+        if (n > 1) S[(e >> 6) * kLd + (e & 63)] /= (float)n;
+    }
+    __syncthreads();
+
+    // g = B1^T . S . B2;  grad = sign(g);  p -= lr * grad   (demo.py:192-209)
+    f32x16 acc = mm64<true, false>(S, B + (int64_t)td.basis2 * 4096);
+    __syncthreads();
+    store_acc(S, acc);
+    __syncthreads();
+    acc = mm64<false, true>(B + (int64_t)td.basis1 * 4096, S);
+    const int cc = acc_col();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int rr = acc_row(r);
+        if (rr < n1 && cc < n2) {
+            const float g = acc[r];
+            const float sg = (float)((g > 0.f) - (g < 0.f));  // torch.sign: NaN -> 0
+            const int64_t a = base + (int64_t)rr * td.cols + cc;
+            for (int64_t k = 0; k < K; ++k) {
+                T* p = param + k * ld + a;
+                Elem<T>::store(p, fmaf(-lr, sg, Elem<T>::load(p)));
+                if (grad) Elem<T>::store(grad + k * ld + a, sg);
+            }
+        }
+    }
+}
+
+static int check_tensors_host(int32_t ntensors, int32_t nchunks) {
+    GA_REQUIRE(ntensors >= 1 && nchunks >= 1, "demo: empty descriptor table (ntensors=%d nchunks=%d)", ntensors,
+               nchunks);
+    return GA_OK;
+}
+
+}  // namespace ga
+
+using namespace ga;
+
+extern "C" GA_API int ga_demo_tensor_bytes(void) { return (int)sizeof(ga_demo_tensor); }
+
+extern "C" GA_API int ga_demo_encode(int dtype, const ga_demo_tensor* tensors, int32_t ntensors, int32_t nchunks,
+                                     const float* F, const float* B, void* param, const void* grad, void* delta,
+                                     int64_t K, int64_t ld, float lr, float decay, float wd_factor,
+                                     int32_t* payload, int64_t payload_stride, int64_t M, hipStream_t stream) {
+    clear_error();
+    if (int e = check_tensors_host(ntensors, nchunks)) return e;
+    GA_REQUIRE(tensors && F && B && param && grad && delta && payload, "ga_demo_encode: null buffer");
+    GA_REQUIRE(K >= 1 && K <= 65535, "ga_demo_encode: K=%lld out of range", (long long)K);
+    GA_REQUIRE(K == 1 || (ld > 0 && payload_stride >= 2 * M), "ga_demo_encode: bad replica strides");
+    dim3 grid((unsigned)nchunks, (unsigned)K);
+    switch (dtype) {
+        case GA_F32:
+            hipLaunchKernelGGL((demo_encode_kernel<float>), grid, dim3(kDmBlock), 0, stream, tensors, ntensors, F, B,
+                               (float*)param, (const float*)grad, (float*)delta, ld, lr, decay, wd_factor, payload,
+                               payload_stride, M);
+            break;
+        case GA_BF16:
+            hipLaunchKernelGGL((demo_encode_kernel<__hip_bfloat16>), grid, dim3(kDmBlock), 0, stream, tensors,
+                               ntensors, F, B, (__hip_bfloat16*)param, (const __hip_bfloat16*)grad,
+                               (__hip_bfloat16*)delta, ld, lr, decay, wd_factor, payload, payload_stride, M);
+            break;
+        default: set_error("ga_demo_encode: unknown dtype %d", dtype); return GA_EINVAL;
+    }
+    return check_launch("ga_demo_encode");
+}
+
+extern "C" GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, int32_t ntensors, int32_t nchunks,
+                                     const float* B, const int32_t* payload, int64_t payload_stride, int64_t M,
+                                     int64_t S, void* param, void* grad, int64_t K, int64_t ld, float lr,
+                                     hipStream_t stream) {
+    clear_error();
+    if (int e = check_tensors_host(ntensors, nchunks)) return e;
+    GA_REQUIRE(tensors && B && payload && param, "ga_demo_decode: null buffer");
+    GA_REQUIRE(S >= 1 && K >= 1, "ga_demo_decode: bad S=%lld K=%lld", (long long)S, (long long)K);
+    GA_REQUIRE(S == 1 || payload_stride >= 2 * M, "ga_demo_decode: payload_stride < 2*M");
+    GA_REQUIRE(K == 1 || ld > 0, "ga_demo_decode: bad ld");
+    switch (dtype) {
+        case GA_F32:
+            hipLaunchKernelGGL((demo_decode_kernel<float>), dim3((unsigned)nchunks), dim3(kDmBlock), 0, stream,
+                               tensors, ntensors, B, payload, payload_stride, M, S, (float*)param, (float*)grad, K,
+                               ld, lr);
+            break;
+        case GA_BF16:
+            hipLaunchKernelGGL((demo_decode_kernel<__hip_bfloat16>), dim3((unsigned)nchunks), dim3(kDmBlock), 0,
+                               stream, tensors, ntensors, B, payload, payload_stride, M, S, (__hip_bfloat16*)param,
+                               (__hip_bfloat16*)grad, K, ld, lr);
+            break;
+        default: set_error("ga_demo_decode: unknown dtype %d", dtype); return GA_EINVAL;
+    }
+    return check_launch("ga_demo_decode");
+}

@@ -1,0 +1,84 @@
+// Shared device helpers and error plumbing for libgym_amd (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "../../include/gym_amd.h"
+
+namespace ga {
+
+// ---- error string (thread local, set by the failing entry point) ----------
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define GA_REQUIRE(cond, ...)                        \
+    do {                                             \
+        if (!(cond)) {                               \
+            ::ga::set_error(__VA_ARGS__);            \
+            return GA_EINVAL;                        \
+        }                                            \
+    } while (0)
+
+// Checks the launch that was just enqueued.
+int check_launch(const char* what);
+
+// ---- element access: arenas are f32 or bf16, arithmetic is f32 ------------
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+    static __device__ __forceinline__ float load(const float* p) { return *p; }
+    static __device__ __forceinline__ void store(float* p, float v) { *p = v; }
+};
+template <> struct Elem<__hip_bfloat16> {
+    static __device__ __forceinline__ float load(const __hip_bfloat16* p) {
+        return __bfloat162float(*p);
+    }
+    static __device__ __forceinline__ void store(__hip_bfloat16* p, float v) {
+        *p = __float2bfloat16(v);  // round to nearest even; NaN stays NaN
+    }
+};
+
+// 16-byte vector of 4 elements for f32, 8-byte for bf16.
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+    using type = float4;
+    static __device__ __forceinline__ void unpack(const float4& v, float (&f)[4]) {
+        f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+    }
+    static __device__ __forceinline__ float4 pack(const float (&f)[4]) {
+        return make_float4(f[0], f[1], f[2], f[3]);
+    }
+};
+template <> struct Vec4<__hip_bfloat16> {
+    using type = uint2;  // 4 x bf16
+    static __device__ __forceinline__ void unpack(const uint2& v, float (&f)[4]) {
+        f[0] = __uint_as_float(v.x << 16);
+        f[1] = __uint_as_float(v.x & 0xffff0000u);
+        f[2] = __uint_as_float(v.y << 16);
+        f[3] = __uint_as_float(v.y & 0xffff0000u);
+    }
+    static __device__ __forceinline__ uint2 pack(const float (&f)[4]) {
+        __hip_bfloat16 b[4];
+        for (int i = 0; i < 4; ++i) b[i] = __float2bfloat16(f[i]);
+        uint2 r;
+        r.x = (uint32_t)__bfloat16_as_ushort(b[0]) | ((uint32_t)__bfloat16_as_ushort(b[1]) << 16);
+        r.y = (uint32_t)__bfloat16_as_ushort(b[2]) | ((uint32_t)__bfloat16_as_ushort(b[3]) << 16);
+        return r;
+    }
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Grid size for a grid-stride streaming kernel: enough workgroups to fill
+// 256 CUs several times over, capped so the tail stays short.
+inline int stream_grid(int64_t work_items, int block) {
+    int64_t g = ceil_div(work_items, block);
+    if (g > 256 * 16) g = 256 * 16;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace ga

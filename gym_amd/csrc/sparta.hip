@@ -1,0 +1,257 @@
+// SPARTA sparse parameter averaging over a flat arena (one launch covers every
+// tensor): select -> gather(sum over local replicas) -> [RCCL all-reduce of
+// the packed values, host side] -> scatter(/divisor) into every replica.
+//
+// Selection is a stream compaction in ascending element order, so the packed
+// order equals `param.data[mask]` over the concatenated parameters
+// (sparta.py:127).  The mask is either a uint8 arena (rank 0's mask, exactly
+// the reference semantics) or generated in-kernel by Philox4x32-10 keyed by
+// (seed, iteration) — then every rank derives the same mask and nothing is
+// broadcast.  Three passes: per-tile count, one-block scan of tile counts,
+// select+gather (the predicate is recomputed; Philox is ~40 integer ops per
+// 4 elements, far below the HBM time of the gather).
+#include "ga_common.h"
+
+namespace ga {
+
+constexpr int kSpBlock = 256;
+constexpr int kSpPerThread = 16;                       // elements per lane
+constexpr int kSpTile = kSpBlock * kSpPerThread;       // 4096 elements per workgroup
+constexpr int kScanBlock = 1024;
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
+        const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += W0;
+        k.y += W1;
+    }
+    return c;
+}
+
+struct Pred {
+    const uint8_t* mask;  // null -> Philox
+    uint2 key;
+    uint32_t it_lo, it_hi, thr;
+};
+
+// Selection bits of the 16 elements starting at element `e0` (e0 % 16 == 0).
+__device__ __forceinline__ uint32_t pred_bits16(const Pred& P, int64_t e0, int64_t n) {
+    uint32_t bits = 0;
+    if (P.mask) {
+        if (e0 + 16 <= n) {
+            const uint4 m = *reinterpret_cast<const uint4*>(P.mask + e0);
+            const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) bits |= (((w[q] >> (8 * b)) & 0xffu) != 0u) << (4 * q + b);
+        } else {
+            for (int j = 0; j < 16 && e0 + j < n; ++j) bits |= (P.mask[e0 + j] != 0) << j;
+        }
+    } else {
+        const uint64_t q0 = (uint64_t)e0 >> 2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t ctr = q0 + q;
+            const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), P.it_lo, P.it_hi), P.key);
+            bits |= ((r.x >> 8) < P.thr) << (4 * q + 0);
+            bits |= ((r.y >> 8) < P.thr) << (4 * q + 1);
+            bits |= ((r.z >> 8) < P.thr) << (4 * q + 2);
+            bits |= ((r.w >> 8) < P.thr) << (4 * q + 3);
+        }
+        if (e0 + 16 > n) bits &= (n - e0) >= 16 ? 0xffffu : ((1u << (uint32_t)(n - e0)) - 1u);
+    }
+    return bits;
+}
+
+// Exclusive scan of one int per lane over a 256-lane workgroup.
+__device__ __forceinline__ int block_excl_scan_256(int v, int* wave_tot, int* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wave_tot[wid] = x;
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int t = wave_tot[w];
+        pre += (w < wid) ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    if (total) *total = tot;
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(kSpBlock) void sparta_count_kernel(Pred P, int64_t n, int32_t* tile_counts) {
+    __shared__ int wave_tot[4];
+    const int64_t e0 = (int64_t)blockIdx.x * kSpTile + (int64_t)threadIdx.x * kSpPerThread;
+    const int c = e0 < n ? __popc(pred_bits16(P, e0, n)) : 0;
+    int total;
+    block_excl_scan_256(c, wave_tot, &total);
+    if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
+}
+
+// One workgroup: exclusive scan of the tile counts -> tile offsets, total and
+// the overflow flag.
+__global__ __launch_bounds__(kScanBlock) void sparta_scan_kernel(const int32_t* tile_counts, int64_t ntiles,
+                                                                 int32_t* tile_offsets, int64_t cap,
+                                                                 int64_t* count) {
+    __shared__ int64_t wave_tot[kScanBlock / 64];
+    const int64_t per = (ntiles + kScanBlock - 1) / kScanBlock;
+    const int64_t b0 = (int64_t)threadIdx.x * per;
+    int64_t s = 0;
+    for (int64_t i = 0; i < per && b0 + i < ntiles; ++i) s += tile_counts[b0 + i];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int64_t x = s;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wave_tot[wid] = x;
+    __syncthreads();
+    int64_t pre = 0, tot = 0;
+    for (int w = 0; w < kScanBlock / 64; ++w) {
+        pre += (w < wid) ? wave_tot[w] : 0;
+        tot += wave_tot[w];
+    }
+    int64_t run = pre + x - s;
+    for (int64_t i = 0; i < per && b0 + i < ntiles; ++i) {
+        tile_offsets[b0 + i] = (int32_t)run;
+        run += tile_counts[b0 + i];
+    }
+    if (threadIdx.x == 0) {
+        count[0] = tot;
+        count[1] = tot > cap ? 1 : 0;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t n, const int32_t* tile_offsets,
+                                                                 const T* __restrict__ src, int64_t K, int64_t ld,
+                                                                 int64_t cap, int32_t* __restrict__ idx,
+                                                                 T* __restrict__ vals) {
+    __shared__ int wave_tot[4];
+    const int64_t e0 = (int64_t)blockIdx.x * kSpTile + (int64_t)threadIdx.x * kSpPerThread;
+    uint32_t bits = e0 < n ? pred_bits16(P, e0, n) : 0u;
+    int pos = block_excl_scan_256(__popc(bits), wave_tot, nullptr) + tile_offsets[blockIdx.x];
+    while (bits) {
+        const int j = __ffs(bits) - 1;
+        bits &= bits - 1;
+        if (pos < cap) {
+            const int64_t i = e0 + j;
+            float acc = 0.f;
+            for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + k * ld + i);
+            idx[pos] = (int32_t)i;
+            Elem<T>::store(vals + pos, acc);
+        }
+        ++pos;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __restrict__ vals,
+                                                                  const int32_t* __restrict__ idx,
+                                                                  const int64_t* __restrict__ count, int64_t cap,
+                                                                  float divisor, T* dst, int64_t K, int64_t ld) {
+    const int64_t m = count[0] < cap ? count[0] : cap;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
+        const float v = Elem<T>::load(vals + j) / divisor;
+        const int64_t i = idx[j];
+        for (int64_t k = 0; k < K; ++k) Elem<T>::store(dst + k * ld + i, v);
+    }
+}
+
+static int64_t sparta_tiles(int64_t n) { return ceil_div(n, kSpTile); }
+
+template <typename T>
+static int launch_select(const void* src, int64_t K, int64_t ld, int64_t n, const Pred& P, int64_t cap,
+                         int32_t* idx, void* vals, int64_t* count, void* work, hipStream_t stream) {
+    const int64_t ntiles = sparta_tiles(n);
+    int32_t* tile_counts = (int32_t*)work;
+    int32_t* tile_offsets = tile_counts + ntiles;
+    hipLaunchKernelGGL(sparta_count_kernel, dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n, tile_counts);
+    if (int e = check_launch("ga_sparta_select(count)")) return e;
+    hipLaunchKernelGGL(sparta_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream, tile_counts, ntiles, tile_offsets,
+                       cap, count);
+    if (int e = check_launch("ga_sparta_select(scan)")) return e;
+    hipLaunchKernelGGL((sparta_select_kernel<T>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
+                       tile_offsets, (const T*)src, K, ld, cap, idx, (T*)vals);
+    return check_launch("ga_sparta_select(gather)");
+}
+
+}  // namespace ga
+
+using namespace ga;
+
+extern "C" GA_API int64_t ga_sparta_workspace_bytes(int64_t n) {
+    return 2 * sparta_tiles(n < 0 ? 0 : n) * (int64_t)sizeof(int32_t) + 256;
+}
+
+extern "C" GA_API uint32_t ga_sparta_threshold(double p) {
+    if (!(p > 0.0)) return 0u;
+    if (p >= 1.0) return 1u << 24;
+    double t = p * 16777216.0;
+    uint32_t u = (uint32_t)t;
+    if ((double)u < t) ++u;  // ceil
+    return u;
+}
+
+extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld, int64_t n,
+                                       const uint8_t* mask, uint64_t seed, uint64_t iteration,
+                                       uint32_t threshold, int64_t cap, int32_t* idx, void* vals,
+                                       int64_t* count, void* work, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "ga_sparta_select: n=%lld out of int32 index range", (long long)n);
+    GA_REQUIRE(K >= 1 && cap >= 0, "ga_sparta_select: bad K=%lld cap=%lld", (long long)K, (long long)cap);
+    GA_REQUIRE(count && work, "ga_sparta_select: null count/work");
+    GA_REQUIRE(K == 1 || ld >= n, "ga_sparta_select: ld < n");
+    GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_select: threshold > 2^24");
+    GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_select: mask must be 16-byte aligned");
+    if (n == 0) return hipMemsetAsync(count, 0, 2 * sizeof(int64_t), stream) == hipSuccess ? GA_OK : GA_EHIP;
+    GA_REQUIRE(src && idx && vals, "ga_sparta_select: null src/idx/vals");
+    Pred P;
+    P.mask = mask;
+    P.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+    P.it_lo = (uint32_t)iteration;
+    P.it_hi = (uint32_t)(iteration >> 32);
+    P.thr = threshold;
+    switch (dtype) {
+        case GA_F32: return launch_select<float>(src, K, ld, n, P, cap, idx, vals, count, work, stream);
+        case GA_BF16: return launch_select<__hip_bfloat16>(src, K, ld, n, P, cap, idx, vals, count, work, stream);
+        default: set_error("ga_sparta_select: unknown dtype %d", dtype); return GA_EINVAL;
+    }
+}
+
+extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx, const int64_t* count,
+                                        int64_t cap, float divisor, void* dst, int64_t K, int64_t ld,
+                                        hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(K >= 1 && cap >= 0, "ga_sparta_scatter: bad K/cap");
+    if (cap == 0) return GA_OK;
+    GA_REQUIRE(vals && idx && count && dst, "ga_sparta_scatter: null buffer");
+    GA_REQUIRE(divisor != 0.0f, "ga_sparta_scatter: divisor is 0");
+    const int grid = stream_grid(cap, kSpBlock);
+    switch (dtype) {
+        case GA_F32:
+            hipLaunchKernelGGL((sparta_scatter_kernel<float>), dim3(grid), dim3(kSpBlock), 0, stream,
+                               (const float*)vals, idx, count, cap, divisor, (float*)dst, K, ld);
+            break;
+        case GA_BF16:
+            hipLaunchKernelGGL((sparta_scatter_kernel<__hip_bfloat16>), dim3(grid), dim3(kSpBlock), 0, stream,
+                               (const __hip_bfloat16*)vals, idx, count, cap, divisor, (__hip_bfloat16*)dst, K, ld);
+            break;
+        default: set_error("ga_sparta_scatter: unknown dtype %d", dtype); return GA_EINVAL;
+    }
+    return check_launch("ga_sparta_scatter");
+}

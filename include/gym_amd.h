@@ -1,0 +1,196 @@
+/*
+ * gym_amd.h — C ABI of the MI355X (gfx950) strategy-communication-step kernels.
+ *
+ * This is the drop-in boundary under EXO Gym's Strategy API (reference:
+ * satoutahhaithem/gym @ 2025-07-11).  Every entry point replaces the per-tensor
+ * torch op loop of one reference function; the replaced interface is cited on
+ * each declaration as `file:line` relative to the reference root.
+ *
+ * Conventions:
+ *   - plain pointers + element counts; no torch types cross this boundary;
+ *   - the caller (PyTorch) owns every buffer: the library never allocates or
+ *     frees device memory and keeps no mutable global state other than a
+ *     thread-local error string;
+ *   - all work is enqueued asynchronously on the given hipStream_t (pass the
+ *     torch current stream); nothing synchronises the host;
+ *   - every function returns 0 on success or a GA_E* code; the message for the
+ *     last failure on the calling thread is available from ga_last_error().
+ *
+ * A "replica set" is K simulated-node copies of one flat parameter arena laid
+ * out as [K, ld] (replica k starts at element k*ld).  K = 1 is the ordinary
+ * one-node-per-GPU case; K > 1 is batched-replica mode.
+ */
+#ifndef GYM_AMD_H
+#define GYM_AMD_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GA_API __attribute__((visibility("default")))
+
+/* error codes */
+#define GA_OK 0
+#define GA_EINVAL 1   /* bad argument (null pointer, bad size, unknown dtype) */
+#define GA_EHIP 2     /* a HIP runtime call or kernel launch failed */
+#define GA_EUNSUP 3   /* unsupported configuration */
+
+/* element types of arena buffers */
+#define GA_F32 0
+#define GA_BF16 1
+
+/* ---- library ---------------------------------------------------------- */
+
+/* ABI version (major*100 + minor). */
+GA_API int ga_abi_version(void);
+
+/* Message describing the last failure on the calling thread ("" if none). */
+GA_API const char* ga_last_error(void);
+
+/* ---- mean reduce: SimpleReduce / FedAvg / DiLoCo averaging ------------- */
+
+/*
+ * dst_j[i] = (sum_{k<K} src[k*ld_src + i]) / divisor   for j < K_out, i < n
+ * (dst_j = dst + j*ld_dst).  Sum in ascending k, fp32 accumulation, then a
+ * correctly rounded true division (reference quirk Q2: division, not *1/K).
+ * If `rows` is non-null it is a device array of K int32 replica indices and
+ * replica rows[k] is read instead of replica k (FedAvg islands).
+ * dst may alias src (in-place all-replica average).  divisor == 1 gives a sum.
+ *
+ * Replaces: exogym/strategy/strategy.py:130-133 (per-param all_reduce + div_),
+ *           exogym/strategy/diloco.py:34-37, exogym/strategy/federated_averaging.py:53-69,
+ *           exogym/trainer.py:95-119 (final state averaging).
+ */
+GA_API int ga_replica_mean(int dtype, const void* src, int64_t K, int64_t ld_src,
+                           const int32_t* rows, int64_t n, float divisor,
+                           void* dst, int64_t K_out, int64_t ld_dst, hipStream_t stream);
+
+/* ---- DiLoCo outer step -------------------------------------------------- */
+
+/*
+ * Fused DiLoCo outer step over n elements (one arena or one shard of it):
+ *   avg  = (sum_{k<K} src_k[i]) / divisor                 (diloco.py:34-37)
+ *   g    = master[i] - avg                                (diloco.py:43-45)
+ *   g   += weight_decay * master[i]          if weight_decay != 0
+ *   buf  = first_step ? g : momentum*buf + (1-dampening)*g   if momentum != 0
+ *   g    = nesterov ? g + momentum*buf : buf                  if momentum != 0
+ *   master[i] -= lr * g                                   (torch SGD, diloco.py:70)
+ *   dst_j[i] = master[i]  for j < K_out                   (diloco.py:47-49 + 39-41)
+ * `mom` may be null when momentum == 0.  master and mom are fp32 when
+ * master_f32 != 0, otherwise they share `dtype` with src/dst.
+ *
+ * Replaces: exogym/strategy/diloco.py:51-76 (the outer-step branch) and the
+ * CPU torch.optim.SGD it drives (diloco.py:26-28,86).
+ */
+GA_API int ga_diloco_outer(int dtype, const void* src, int64_t K, int64_t ld_src,
+                           int64_t n, float divisor, void* master, void* mom,
+                           int master_f32, int first_step, float lr, float momentum,
+                           float dampening, float weight_decay, int nesterov,
+                           void* dst, int64_t K_out, int64_t ld_dst, hipStream_t stream);
+
+/* ---- SPARTA sparse averaging ------------------------------------------- */
+
+/* Workspace bytes needed by ga_sparta_select for an arena of n elements. */
+GA_API int64_t ga_sparta_workspace_bytes(int64_t n);
+
+/* Selection threshold used by the Philox mask: select iff (u32 >> 8) < thr. */
+GA_API uint32_t ga_sparta_threshold(double p);
+
+/*
+ * Select the SPARTA index set over an arena of n elements and gather the
+ * selected values summed over the K local replicas.
+ *   mask source: if mask != null, element i is selected iff mask[i] != 0
+ *   (uint8 mask, rank 0's mask broadcast — sparta.py:121-126); otherwise the
+ *   in-kernel Philox4x32-10 stream decides: select iff
+ *   (philox(key=seed, ctr={i/4, iteration})[i%4] >> 8) < threshold.
+ * Outputs (device): idx[j] = j-th selected element index in ascending order
+ * (row-major over the arena, == param.data[mask] order, sparta.py:127),
+ * vals[j] = sum_k src_k[idx[j]], count[0] = number selected (int64),
+ * count[1] = 1 if that exceeded `cap` (only the first cap are written).
+ * `work` must hold ga_sparta_workspace_bytes(n) bytes.
+ *
+ * Replaces: RandomIndexSelector.get_indices (sparta.py:169-174), the mask
+ * broadcast and gather of SparseCommunicator.communicate (sparta.py:113-131).
+ */
+GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld,
+                            int64_t n, const uint8_t* mask, uint64_t seed,
+                            uint64_t iteration, uint32_t threshold, int64_t cap,
+                            int32_t* idx, void* vals, int64_t* count, void* work,
+                            hipStream_t stream);
+
+/*
+ * dst_k[idx[j]] = vals[j] / divisor for j < min(count[0], cap), k < K.
+ * Replaces: `sparse_data /= num_nodes; param.masked_scatter_(mask, sparse_data)`
+ * (sparta.py:129-131).
+ */
+GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
+                             const int64_t* count, int64_t cap, float divisor,
+                             void* dst, int64_t K, int64_t ld, hipStream_t stream);
+
+/* ---- DeMo DCT codec ------------------------------------------------------ */
+
+/*
+ * One parameter tensor as the DeMo codec sees it: a 2-D [rows, cols] view of
+ * the arena at `offset` (1-D [L] -> [1, L] with n1 = 1; 4-D [b,c,h,w] ->
+ * [b*c*h, w] with n1 = h, n2 = w), cut into gy x gx chunks of n1 x n2
+ * (demo_impl/demo.py:255-276).  Each chunk sends k entries
+ * (k = clamp(topk, 1, n1*n2), demo.py:307-323) stored at payload entry
+ * payload_off + chunk*k.  basis1/basis2 index the 64x64 basis tables
+ * (zero padded; n = 1 is the identity).  chunk_start is the prefix sum of
+ * gy*gx over the descriptor table.
+ */
+typedef struct ga_demo_tensor {
+    int64_t offset;
+    int64_t payload_off;
+    int32_t rows, cols;
+    int32_t n1, n2;
+    int32_t gy, gx;
+    int32_t k;
+    int32_t basis1, basis2;
+    int32_t chunk_start;
+} ga_demo_tensor;
+
+/* sizeof(ga_demo_tensor) as compiled into the library (ABI check for bindings). */
+GA_API int ga_demo_tensor_bytes(void);
+
+/*
+ * Encode + compress + residual for every chunk of every tensor, for each of
+ * K replicas (replica r: param/grad/delta at + r*ld, payload at + r*payload_stride):
+ *   p     *= wd_factor                      if wd_factor != 1 (demo.py:159-160; the
+ *                                           caller passes 1 - lr*weight_decay computed
+ *                                           in double, as the reference's Python scalar)
+ *   delta  = decay*delta + lr*grad          (demo.py:163-167)
+ *   Y      = F1^T . delta_chunk . F2        (DCT-II, demo.py:255-276; fp32 MFMA)
+ *   top-k of |Y| per chunk                   (demo.py:315-328; ties: lowest index)
+ *   delta -= B1^T . S . B2                  (S = the k kept coefficients, demo.py:174-180)
+ * Payload per replica: idx int32[M] then val f32[M] (M = total entries), entries
+ * of one chunk in ascending coefficient index.  F/B tables: [nbasis][64][64] fp32.
+ */
+GA_API int ga_demo_encode(int dtype, const ga_demo_tensor* tensors, int32_t ntensors,
+                          int32_t nchunks, const float* F, const float* B,
+                          void* param, const void* grad, void* delta, int64_t K,
+                          int64_t ld, float lr, float decay, float wd_factor,
+                          int32_t* payload, int64_t payload_stride, int64_t M,
+                          hipStream_t stream);
+
+/*
+ * Decode the gathered payloads of S sources (source s at payload + s*payload_stride,
+ * in node order), scatter-mean them per chunk (mean over the entries that hit a
+ * coefficient, demo.py:331-352), inverse DCT (B1^T . X . B2), sign, and apply the
+ * SGD step to each of K local replicas:  grad = sign(g);  p -= lr*grad
+ * (demo.py:192-209).  grad may be null (then only p is written).
+ */
+GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, int32_t ntensors,
+                          int32_t nchunks, const float* B, const int32_t* payload,
+                          int64_t payload_stride, int64_t M, int64_t S, void* param,
+                          void* grad, int64_t K, int64_t ld, float lr,
+                          hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GYM_AMD_H */

@@ -1,0 +1,122 @@
+"""SPARTA sparse averaging and the selector masks (oracle; test infrastructure only).
+
+Reference: SparseCommunicator.communicate (exogym/strategy/sparta.py:113-131):
+  mask = rank 0's index_selector.get_indices(param, iteration)   (:121-126, broadcast)
+  v = param.data[mask]            row-major order over the tensor (:127)
+  v = (sum_k v_k) / num_nodes     all_reduce SUM then true division (:128-129)
+  param.masked_scatter_(mask, v)  (:131)
+Selectors restated given their torch random draws as inputs:
+  ShuffledSequentialIndexSelector (:177-225), PartitionedIndexSelector (:228-282).
+
+gym_amd's fast mask mode has no reference counterpart: it draws the mask from
+Philox4x32-10 (Salmon et al., SC'11, "Parallel random numbers: as easy as
+1, 2, 3"; constants as in Random123) keyed by (seed, iteration) over the flat
+arena index.  `philox4x32_10` restates that generator; it is pinned by the
+Random123 known-answer vectors in tests/test_oracle_golden.py.
+"""
+import math
+
+import numpy as np
+
+from .reduce import mean_reduce
+
+M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+W0, W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(ctr, key):
+    """ctr: uint32 array [..., 4]; key: uint32 array [..., 2] (broadcastable)."""
+    c = [np.asarray(ctr[..., i], dtype=np.uint32) for i in range(4)]
+    k0 = np.asarray(key[..., 0], dtype=np.uint32)
+    k1 = np.asarray(key[..., 1], dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        return _philox_rounds(c, k0, k1)
+
+
+def _philox_rounds(c, k0, k1):
+    for _ in range(10):
+        p0 = c[0].astype(np.uint64) * M0
+        p1 = c[2].astype(np.uint64) * M1
+        hi0, lo0 = (p0 >> np.uint64(32)).astype(np.uint32), (p0 & MASK32).astype(np.uint32)
+        hi1, lo1 = (p1 >> np.uint64(32)).astype(np.uint32), (p1 & MASK32).astype(np.uint32)
+        c = [hi1 ^ c[1] ^ k0, lo1, hi0 ^ c[3] ^ k1, lo0]
+        k0 = (k0 + W0).astype(np.uint32)
+        k1 = (k1 + W1).astype(np.uint32)
+    return np.stack(c, axis=-1)
+
+
+def threshold(p):
+    """Integer threshold: select iff (u32 >> 8) < threshold(p) (P = thr / 2^24)."""
+    if not p > 0.0:
+        return 0
+    if p >= 1.0:
+        return 1 << 24
+    return int(math.ceil(p * 16777216.0))
+
+
+def philox_mask(n, seed, iteration, p, start=0):
+    """Mask bits of arena elements [start, start+n) for (seed, iteration)."""
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    q = idx >> np.uint64(2)
+    ctr = np.stack([(q & MASK32).astype(np.uint32), (q >> np.uint64(32)).astype(np.uint32),
+                    np.full(n, iteration & 0xFFFFFFFF, np.uint32),
+                    np.full(n, (iteration >> 32) & 0xFFFFFFFF, np.uint32)], axis=-1)
+    key = np.array([seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF], dtype=np.uint32)
+    words = philox4x32_10(ctr, key)
+    lane = (idx & np.uint64(3)).astype(np.int64)
+    w = words[np.arange(n), lane]
+    return (w >> np.uint32(8)) < np.uint32(threshold(p))
+
+
+def sparse_average(node_params, mask, divisor=None):
+    """node_params: list of K arrays of one tensor; mask: bool array of the same
+    shape.  Returns the K updated arrays (sparta.py:127-131)."""
+    flat_mask = np.asarray(mask, dtype=bool).reshape(-1)
+    vals = [np.asarray(p, dtype=np.float32).reshape(-1)[flat_mask] for p in node_params]
+    avg = mean_reduce(vals, divisor if divisor is not None else len(node_params))
+    out = []
+    for p in node_params:
+        q = np.asarray(p, dtype=np.float32).reshape(-1).copy()
+        q[flat_mask] = avg
+        out.append(q.reshape(np.shape(p)))
+    return out
+
+
+def selected_indices(mask):
+    """param.data[mask] order: ascending flat index."""
+    return np.flatnonzero(np.asarray(mask).reshape(-1))
+
+
+def shuffled_sequential_mask(numel, p, shuffled_indices, iteration):
+    """ShuffledSequentialIndexSelector.get_indices (sparta.py:184-225) given the
+    tensor's randperm drawn on first use."""
+    if numel == 0:
+        return np.zeros(0, dtype=bool)
+    num_partitions = max(1, math.ceil(1.0 / p))
+    chunk = iteration % num_partitions
+    size, rem = divmod(numel, num_partitions)
+    start = chunk * size + min(chunk, rem)
+    end = start + size + (1 if chunk < rem else 0)
+    m = np.zeros(numel, dtype=bool)
+    m[np.asarray(shuffled_indices)[start:end]] = True
+    return m
+
+
+def partitioned_masks(numel, p, rank_orders, calls):
+    """PartitionedIndexSelector.get_indices (sparta.py:235-282) for `calls`
+    consecutive calls on one tensor, given the orders torch.rand(numel).argsort()
+    produced at each (re)partition (rank_orders[j] for the j-th; argsort's order
+    among tied draws is torch's, so it is an input here, like the randperm of
+    the shuffled selector)."""
+    nparts = max(1, min(math.ceil(1.0 / p), numel))
+    out, cur, draw = [], None, 0
+    parts = None
+    for _ in range(calls):
+        if parts is None or cur >= nparts:
+            parts = np.asarray(rank_orders[draw]) % nparts
+            draw += 1
+            cur = 0
+        out.append(parts == cur)
+        cur += 1
+    return out
