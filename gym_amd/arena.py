@@ -1,0 +1,142 @@
+"""Flat parameter arenas.
+
+One simulated node's parameters live in ONE contiguous buffer so a single
+kernel launch (and a single RCCL call) covers every tensor, instead of the
+reference's per-tensor loops (e.g. strategy.py:130-133, diloco.py:34-41,
+sparta.py:117-131).  Tensor offsets are aligned to 64 elements (256 B for
+fp32) so every tensor starts on a cache line and 16-byte vector loads stay
+aligned; the padding between tensors is kept at zero, so elementwise kernels
+may run over the whole arena.
+
+ArenaLayout   offsets of an ordered shape list (+ the padded arena length)
+ReplicaSet    K replicas of a layout as one [K, ld] tensor (batched-replica mode)
+ParamArena    re-points an nn.Module's parameters (and their .grad) at views
+              of a flat buffer, keeping `model.parameters()` / `state_dict()`
+              keys and shapes unchanged
+"""
+import math
+
+import torch
+
+ALIGN = 64  # elements
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+class ArenaLayout:
+    def __init__(self, shapes, align=ALIGN, shard_multiple=8):
+        self.shapes = [tuple(int(d) for d in s) for s in shapes]
+        self.numels = [int(math.prod(s)) for s in self.shapes]
+        self.offsets = []
+        off = 0
+        for n in self.numels:
+            self.offsets.append(off)
+            off = _round_up(off + n, align)
+        self.n_params = sum(self.numels)
+        # padded so [n] splits into `shard_multiple` aligned shards (reduce-scatter)
+        self.n = max(_round_up(off, align * shard_multiple), align * shard_multiple)
+
+    def __len__(self):
+        return len(self.shapes)
+
+    def views(self, flat):
+        """Per-tensor views of a flat [>= n] buffer."""
+        return [flat[o:o + n].view(s) for o, n, s in zip(self.offsets, self.numels, self.shapes)]
+
+    def shard(self, rank, world):
+        """[begin, end) of rank's shard for a world-size split (aligned)."""
+        per = _round_up(-(-self.n // world), ALIGN)
+        b = min(rank * per, self.n)
+        return b, min(b + per, self.n)
+
+    def padded_to(self, world):
+        per = _round_up(-(-self.n // world), ALIGN)
+        return per * world
+
+
+class ReplicaSet:
+    """K simulated-node replicas of one arena: data[k] is replica k."""
+
+    def __init__(self, layout, K, device, dtype=torch.float32, ld=None, fill=None):
+        self.layout = layout
+        self.K = int(K)
+        self.ld = int(ld or layout.n)
+        self.data = torch.zeros(self.K, self.ld, device=device, dtype=dtype) if fill is None else fill
+        assert self.data.shape == (self.K, self.ld)
+
+    def replica(self, k):
+        return self.data[k]
+
+    def views(self, k):
+        return self.layout.views(self.data[k])
+
+
+class ParamArena:
+    """Binds the parameters of a module (or a parameter list) to one flat
+    buffer and their gradients to another.  Parameters without
+    requires_grad are still placed (they keep their values) but get no grad."""
+
+    def __init__(self, params, device=None, dtype=None, world=1, with_grad=True):
+        self.params = [p for p in params]
+        if not self.params:
+            raise ValueError("ParamArena: empty parameter list")
+        self.device = device or self.params[0].device
+        self.dtype = dtype or self.params[0].dtype
+        for p in self.params:
+            if p.dtype != self.dtype:
+                raise TypeError(f"ParamArena: mixed parameter dtypes ({p.dtype} vs {self.dtype})")
+        self.layout = ArenaLayout([p.shape for p in self.params])
+        n = self.layout.padded_to(world)
+        self.flat = torch.zeros(n, device=self.device, dtype=self.dtype)
+        self.grad_flat = torch.zeros(n, device=self.device, dtype=self.dtype) if with_grad else None
+        with torch.no_grad():
+            for p, v in zip(self.params, self.layout.views(self.flat)):
+                v.copy_(p.data)
+                p.data = v
+        self._data_ptrs = [p.data_ptr() for p in self.params]
+        self._grad_views = None
+        if with_grad:
+            self._grad_views = self.layout.views(self.grad_flat)
+            for p, g in zip(self.params, self._grad_views):
+                if p.requires_grad:
+                    if p.grad is not None:
+                        g.copy_(p.grad)
+                    p.grad = g
+
+    @property
+    def n(self):
+        return self.flat.numel()
+
+    def check_bound(self):
+        """Raise if something re-pointed a parameter away from the arena
+        (e.g. `param.data = ...`), which would silently desynchronise it."""
+        if [p.data_ptr() for p in self.params] != self._data_ptrs:
+            raise RuntimeError("ParamArena: a parameter's storage was replaced outside the arena; "
+                               "update parameters in place (param.data.copy_) instead")
+
+    def sync_grads(self):
+        """Make sure every .grad is the arena view (autograd allocates a fresh
+        tensor when .grad was None, e.g. after zero_grad(set_to_none=True)):
+        copy such grads into the arena and re-point them."""
+        if self._grad_views is None:
+            return
+        for p, g in zip(self.params, self._grad_views):
+            if not p.requires_grad:
+                continue
+            cur = p.grad
+            if cur is g:
+                continue
+            if cur is None:
+                g.zero_()
+            elif cur.data_ptr() != g.data_ptr():
+                g.copy_(cur)
+            p.grad = g
+
+    def zero_grad(self):
+        if self.grad_flat is not None:
+            self.grad_flat.zero_()
+            for p, g in zip(self.params, self._grad_views):
+                if p.requires_grad:
+                    p.grad = g

@@ -1,0 +1,73 @@
+"""Collectives on flat arenas.
+
+Replaces the per-tensor wrappers of exogym/strategy/communicate.py:63-75: the
+strategies here issue ONE collective per step over a whole arena (or a whole
+packed payload), on the process group set up one process per GPU with the
+"nccl" backend, which is RCCL over xGMI on ROCm.  The gloo backend (CPU tests,
+or several nodes sharing a GPU) is supported with the same semantics: gloo has
+no reduce-scatter, so those paths fall back to all-reduce.
+"""
+import torch
+import torch.distributed as dist
+
+
+class Collective:
+    def __init__(self, group=None):
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+            self.backend = str(dist.get_backend(group)).lower()
+        else:
+            self.world, self.rank, self.backend = 1, 0, "none"
+
+    @property
+    def rccl(self):
+        return self.backend == "nccl"
+
+    # -- collectives (no-ops at world size 1) --------------------------------
+    def all_reduce_(self, t):
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def broadcast_(self, t, src=0):
+        if self.world > 1:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def reduce_scatter(self, shard_out, full):
+        """shard_out = rank's shard of sum over ranks of `full` (full is scratch:
+        the gloo fallback reduces it in place)."""
+        if self.world == 1:
+            if shard_out.data_ptr() != full.data_ptr():
+                shard_out.copy_(full[: shard_out.numel()])
+            return shard_out
+        if self.rccl:
+            dist.reduce_scatter_tensor(shard_out, full, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group)
+            per = shard_out.numel()
+            shard_out.copy_(full[self.rank * per:(self.rank + 1) * per])
+        return shard_out
+
+    def all_gather_into(self, full, shard):
+        """full[r*per:(r+1)*per] = shard of rank r.  `shard` may be the rank's
+        own slice of `full` (in place)."""
+        if self.world == 1:
+            if full.data_ptr() != shard.data_ptr():
+                full[: shard.numel()].copy_(shard)
+            return full
+        if self.rccl:
+            dist.all_gather_into_tensor(full, shard, group=self.group)
+        else:
+            per = shard.numel()
+            parts = list(full.split(per))
+            src = shard.clone() if shard.data_ptr() == parts[self.rank].data_ptr() else shard
+            dist.all_gather(parts, src, group=self.group)
+        return full
+
+
+def world_and_rank(group=None):
+    c = Collective(group)
+    return c.world, c.rank

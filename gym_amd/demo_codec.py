@@ -1,0 +1,129 @@
+"""Host-side plan for the DeMo DCT codec kernels (ga_demo_encode / ga_demo_decode).
+
+Built once per arena layout (the analogue of TransformDCT.__init__,
+exogym/strategy/demo_impl/demo.py:214-236): per tensor, the 2-D view and
+chunk sizes chosen by `_get_smaller_split` (demo.py:489-498), the per-chunk
+entry count k = clamp(topk, 1, n1*n2) (demo.py:307-312), the payload offsets,
+and the DCT-II / inverse bases as zero-padded 64x64 fp32 tables.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from ._lib import DemoTensor
+
+TILE = 64
+
+
+def _prime_factors(n):
+    f, d = [], 2
+    while d * d <= n:
+        while n % d == 0:
+            f.append(d)
+            n //= d
+        d += 1
+    if n > 1:
+        f.append(n)
+    return f
+
+
+def smaller_split(n, target):
+    """Chunk size for a dimension of size n (demo.py:489-498): `target` if it
+    divides n, else the largest divisor below target; if 1 already exceeds
+    target, the smallest divisor; n when every divisor is below target."""
+    divs = {1}
+    for p in _prime_factors(n):
+        divs |= {d * p for d in divs}
+    ds = sorted(divs)
+    prev = None
+    for v in ds:
+        if v == target:
+            return v
+        if v > target:
+            return v if prev is None else prev
+        prev = v
+    return n
+
+
+def codec_view(shape, chunk):
+    """(rows, cols, n1, n2) of the 2-D view the codec uses for a parameter."""
+    shape = tuple(int(s) for s in shape)
+    if len(shape) == 1:
+        return 1, shape[0], 1, smaller_split(shape[0], chunk)
+    if len(shape) == 2:
+        return shape[0], shape[1], smaller_split(shape[0], chunk), smaller_split(shape[1], chunk)
+    if len(shape) == 4:  # conv kernels: full DCT over (h, w) per (out, in) pair (demo.py:256-260)
+        b, c, h, w = shape
+        if smaller_split(h, chunk) != h or smaller_split(w, chunk) != w:
+            raise ValueError(f"DeMo: 4-D parameter {shape} needs its spatial dims to be whole chunks")
+        return b * c * h, w, h, w
+    raise ValueError(f"DeMo: parameters of rank {len(shape)} are not supported (shape {shape})")
+
+
+def dct_table(n):
+    """F[i, k] = c_k cos(pi (2i+1) k / 2n): the ortho DCT-II basis the reference
+    builds as _dct(eye(n), 'ortho') (demo.py:364-395), spatial i, frequency k."""
+    i = np.arange(n)[:, None]
+    k = np.arange(n)[None, :]
+    c = np.where(k == 0, math.sqrt(1.0 / n), math.sqrt(2.0 / n))
+    return c * np.cos(math.pi * (2 * i + 1) * k / (2 * n))
+
+
+class DemoPlan:
+    def __init__(self, layout, chunk=64, topk=32):
+        self.layout = layout
+        self.chunk = int(chunk)
+        self.topk = int(topk)
+        sizes, descs = [], []
+        basis_of = {}
+        payload_off = 0
+        chunk_start = 0
+        self.entries_per_tensor = []
+        for shape, off in zip(layout.shapes, layout.offsets):
+            R, C, n1, n2 = codec_view(shape, self.chunk)
+            if n1 > TILE or n2 > TILE:
+                raise NotImplementedError(f"DeMo chunk {n1}x{n2} > {TILE}x{TILE} (compression_chunk <= 64)")
+            for n in (n1, n2):
+                if n not in basis_of:
+                    basis_of[n] = len(sizes)
+                    sizes.append(n)
+            gy, gx = R // n1, C // n2
+            k = max(1, min(self.topk, n1 * n2))
+            d = DemoTensor(offset=off, payload_off=payload_off, rows=R, cols=C, n1=n1, n2=n2, gy=gy, gx=gx, k=k,
+                           basis1=basis_of[n1], basis2=basis_of[n2], chunk_start=chunk_start)
+            descs.append(d)
+            self.entries_per_tensor.append(gy * gx * k)
+            payload_off += gy * gx * k
+            chunk_start += gy * gx
+        if chunk_start >= 2**31:
+            raise ValueError("DeMo: too many chunks for one launch")
+        self.ntensors = len(descs)
+        self.nchunks = chunk_start
+        self.M = payload_off
+        self.n_arena = layout.n
+        arr = (DemoTensor * len(descs))(*descs)
+        self._desc_host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        F = np.zeros((len(sizes), TILE, TILE), np.float64)
+        for j, n in enumerate(sizes):
+            F[j, :n, :n] = dct_table(n)
+        self._F_host = torch.from_numpy(F.astype(np.float32))
+        # the inverse of an orthonormal basis is its transpose (idct(eye(n)), demo.py:398-442)
+        self._B_host = torch.from_numpy(np.ascontiguousarray(F.transpose(0, 2, 1)).astype(np.float32))
+        self.basis_sizes = sizes
+        self.device = None
+        self.desc = self.F = self.B = None
+
+    def to(self, device):
+        device = torch.device(device)
+        if self.device != device:
+            self.desc = self._desc_host.to(device)
+            self.F = self._F_host.to(device)
+            self.B = self._B_host.to(device)
+            self.device = device
+        return self
+
+    def reference_bytes(self, val_itemsize=4):
+        """DeMo.data_transmit of the reference for one step (int64 idx + value)."""
+        return self.M * (8 + val_itemsize)

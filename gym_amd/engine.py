@@ -1,0 +1,209 @@
+"""Flat step bodies: the strategy communication step over [K_local, ld]
+replica sets, one kernel (plus at most one collective per exchange) per step.
+
+Each engine is used by the Strategy API classes (K_local = 1: one simulated
+node per process/GPU) and directly by the bench for batched-replica mode
+(K_local > 1 simulated nodes on one GPU, reduced over K in-kernel before the
+cross-GPU exchange).  World = number of processes in the collective; the
+node count is K_total = world * K_local.
+
+  MeanReduce   SimpleReduce grads, FedAvg params     strategy.py:128-142, federated_averaging.py:53-69
+  DiLoCoOuter  fused outer SGD/Nesterov step        diloco.py:34-76
+  Sparta       sparse average (Philox or mask)      sparta.py:113-131
+  DeMoCodec    DCT encode/top-k + gather + decode   demo_impl/demo.py:142-209
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from .comm import Collective
+from .demo_codec import DemoPlan
+
+
+def _f32(x):
+    return float(np.float32(x))
+
+
+class MeanReduce:
+    """Every replica <- (sum over all K_total nodes) / K_total."""
+
+    def __init__(self, coll: Collective, K_local, n, device, dtype):
+        self.coll, self.K_local, self.n = coll, int(K_local), int(n)
+        self.K_total = coll.world * self.K_local
+        self.sum = torch.empty(n, device=device, dtype=dtype) if (coll.world > 1 and K_local > 1) else None
+
+    def __call__(self, reps):
+        K, n = self.K_local, self.n
+        if self.coll.world == 1:
+            if K > 1:
+                ops.replica_mean(reps, reps, n=n)
+            return
+        if K == 1:
+            self.coll.all_reduce_(reps[0, :n])
+            ops.replica_mean(reps[0:1], reps[0:1], n=n, divisor=self.K_total)
+        else:
+            ops.replica_mean(reps, self.sum, n=n, divisor=1.0)
+            self.coll.all_reduce_(self.sum)
+            ops.replica_mean(self.sum, reps, n=n, divisor=self.K_total)
+
+
+class DiLoCoOuter:
+    """Fused DiLoCo outer step.  With RCCL and world > 1 the master copy and
+    the momentum are sharded: reduce-scatter(sum) -> fused update of the own
+    shard -> all-gather(params); the same bytes on the wire as the reference's
+    all-reduce + broadcast, the outer-optimizer state / G per GPU."""
+
+    def __init__(self, coll: Collective, K_local, n, device, dtype, lr=0.7, momentum=0.9, nesterov=True,
+                 dampening=0.0, weight_decay=0.0, shard=None):
+        self.coll, self.K_local = coll, int(K_local)
+        self.K_total = coll.world * self.K_local
+        self.hp = dict(lr=lr, momentum=momentum, nesterov=nesterov, dampening=dampening, weight_decay=weight_decay)
+        W = coll.world
+        self.shard = (coll.rccl and W > 1) if shard is None else (shard and W > 1)
+        self.n = int(n)
+        if self.shard:
+            assert n % W == 0, "arena must be padded to a multiple of the world size"
+            self.per = n // W
+            self.lo = coll.rank * self.per
+            self.hi = self.lo + self.per
+        else:
+            self.per, self.lo, self.hi = n, 0, n
+        self.master = torch.zeros(self.per, device=device, dtype=torch.float32)
+        self.mom = torch.zeros(self.per, device=device, dtype=torch.float32) if momentum != 0 else None
+        self.first = True
+        self.dtype = dtype
+        needs_sum = W > 1 and (self.K_local > 1 or not self.shard)
+        self.sum = torch.empty(n, device=device, dtype=dtype) if needs_sum else None
+        self.rs_out = torch.empty(self.per, device=device, dtype=dtype) if self.shard else None
+        self.gather = torch.empty(n, device=device, dtype=dtype) if (self.shard and self.K_local > 1) else None
+
+    def init_master(self, params_flat):
+        """master <- the node's initial parameters (diloco.py:81-82)."""
+        self.master.copy_(params_flat[self.lo:self.hi])
+        self.first = True
+
+    def _outer(self, src, divisor, dst):
+        h = self.hp
+        ops.diloco_outer(src, self.master, self.mom, dst, self.per, divisor, h["lr"], h["momentum"], h["dampening"],
+                         h["weight_decay"], h["nesterov"], self.first)
+        self.first = False
+
+    def __call__(self, reps):
+        n, K = self.n, self.K_local
+        W = self.coll.world
+        if W == 1:  # one kernel: read every replica, update, write every replica
+            self._outer(reps[:, :n], self.K_total, reps[:, :n])
+            return
+        if not self.shard:  # gloo: all-reduce the sum, replicated update
+            ops.replica_mean(reps, self.sum, n=n, divisor=1.0)
+            self.coll.all_reduce_(self.sum)
+            self._outer(self.sum, self.K_total, reps[:, :n])
+            return
+        src_full = reps[0, :n] if K == 1 else self.sum
+        if K > 1:
+            ops.replica_mean(reps, self.sum, n=n, divisor=1.0)
+        self.coll.reduce_scatter(self.rs_out, src_full)
+        if K == 1:
+            own = reps[0, self.lo:self.hi]
+            self._outer(self.rs_out, self.K_total, own)
+            self.coll.all_gather_into(reps[0, :n], own)
+        else:
+            own = self.gather[self.lo:self.hi]
+            self._outer(self.rs_out, self.K_total, own)
+            self.coll.all_gather_into(self.gather, own)
+            ops.replica_mean(self.gather, reps, n=n, divisor=1.0)
+
+
+def sparta_capacity(n, p):
+    """Packed-value capacity for a Philox draw of n elements at rate p: mean +
+    16 sigma + 1024 (overflow is flagged on the device and raised by check())."""
+    mu = n * p
+    return int(min(n, math.ceil(mu + 16.0 * math.sqrt(max(mu * (1 - p), 1.0)) + 1024)))
+
+
+class Sparta:
+    """SPARTA sparse averaging over the whole arena in one select/gather, one
+    all-reduce of the packed values, one scatter."""
+
+    def __init__(self, coll: Collective, K_local, n, device, dtype, p):
+        self.coll, self.K_local, self.n, self.p = coll, int(K_local), int(n), float(p)
+        self.K_total = coll.world * self.K_local
+        self.device, self.dtype = device, dtype
+        self.cap = sparta_capacity(n, self.p)
+        self.idx = torch.empty(self.cap, dtype=torch.int32, device=device)
+        self.vals = torch.empty(self.cap, dtype=dtype, device=device)
+        self.count = torch.zeros(2, dtype=torch.int64, device=device)
+        self.work = ops.sparta_workspace(n, device)
+        self._flag_host = torch.zeros(2, dtype=torch.int64, pin_memory=torch.cuda.is_available())
+        self._flag_event = None
+
+    def _ensure_cap(self, cap):
+        if cap > self.cap:
+            self.cap = cap
+            self.idx = torch.empty(cap, dtype=torch.int32, device=self.device)
+            self.vals = torch.empty(cap, dtype=self.dtype, device=self.device)
+
+    def check(self):
+        """Raise if an earlier Philox step selected more than the capacity."""
+        if self._flag_event is not None:
+            self._flag_event.synchronize()
+            if int(self._flag_host[1]) != 0:
+                raise RuntimeError(f"SPARTA: {int(self._flag_host[0])} elements selected > capacity {self.cap}")
+
+    def __call__(self, reps, seed=0, iteration=0, mask=None):
+        n = self.n
+        if mask is not None:  # reference mask (rank 0's); exact count known from the mask
+            cap = max(1, int(mask[:n].sum().item()))
+            self._ensure_cap(cap)
+            cap_used = cap
+        else:
+            self.check()
+            cap_used = self.cap
+        ops.sparta_select(reps, n, cap_used, self.idx, self.vals, self.count, self.work, mask=mask, seed=seed,
+                          iteration=iteration, p=self.p)
+        self.coll.all_reduce_(self.vals[:cap_used])
+        ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps)
+        if mask is None:
+            self._flag_host.copy_(self.count, non_blocking=True)
+            self._flag_event = torch.cuda.Event()
+            self._flag_event.record()
+
+
+class DeMoCodec:
+    """DeMo step: encode every replica's delta (DCT + top-k + residual), one
+    all-gather of the packed payloads, decode + sign-SGD applied to every
+    replica.  Payload per node: int32 idx[M] then fp32 val[M]."""
+
+    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32):
+        self.coll, self.K_local = coll, int(K_local)
+        self.K_total = coll.world * self.K_local
+        self.plan = DemoPlan(layout, chunk=chunk, topk=topk).to(device)
+        M = self.plan.M
+        self.payload = torch.zeros(self.K_local, 2 * M, dtype=torch.int32, device=device)
+        self.gathered = (torch.zeros(self.K_total, 2 * M, dtype=torch.int32, device=device)
+                         if coll.world > 1 else self.payload)
+
+    def encode(self, P, G, D, lr, decay, weight_decay):
+        wdf = _f32(1.0 - lr * weight_decay) if weight_decay != 0.0 else 1.0
+        ops.demo_encode(self.plan, P, G, D, self.payload, _f32(lr), _f32(decay), wdf)
+
+    def exchange(self, all_gather=None):
+        if self.coll.world == 1:
+            return
+        if all_gather is None:
+            self.coll.all_gather_into(self.gathered.view(-1), self.payload.view(-1))
+        else:  # a user-supplied list-style all_gather (DeMo(custom_all_gather=...))
+            parts = list(self.gathered.view(self.coll.world, -1).unbind(0))
+            h = all_gather(parts, self.payload.view(-1), group=self.coll.group, async_op=True)
+            if h is not None and hasattr(h, "wait"):
+                h.wait()
+
+    def decode(self, P, G, lr):
+        ops.demo_decode(self.plan, self.gathered, P, G, _f32(lr))
+
+    def __call__(self, P, G, D, lr, decay=0.999, weight_decay=0.0, all_gather=None):
+        self.encode(P, G, D, lr, decay, weight_decay)
+        self.exchange(all_gather)
+        self.decode(P, G, lr)

@@ -1,0 +1,174 @@
+"""Tensor-level wrappers of the gfx950 kernels (libgym_amd.so).
+
+Every function takes torch tensors that live on the GPU, checks shapes and
+dtypes on the host (so a kernel never runs on operands it was not sized for),
+and enqueues the kernel on torch's current stream.  There is no CPU path:
+a CPU tensor raises.
+
+Replica sets are 2-D tensors [K, ld]; a 1-D tensor is one replica.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import DemoTensor, check, lib
+
+_DT = {torch.float32: _lib.GA_F32, torch.bfloat16: _lib.GA_BF16}
+
+
+def _dtype_code(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"gym_amd: unsupported dtype {t.dtype} (float32 / bfloat16)") from None
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("gym_amd kernels run on the MI355X only: got a CPU tensor (there is no CPU fallback)")
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _as2d(t):
+    return t if t.dim() == 2 else t.view(1, -1)
+
+
+def _rows_ld(t2):
+    assert t2.dim() == 2
+    if t2.shape[0] > 1 and t2.stride(1) != 1:
+        raise ValueError("replica set must be row-major contiguous")
+    return t2.shape[0], (t2.stride(0) if t2.shape[0] > 1 else t2.shape[1])
+
+
+def replica_mean(src, dst, n=None, divisor=None, rows=None):
+    """dst[j, :n] = (sum_k src[k, :n]) / divisor for every row j of dst
+    (divisor defaults to the number of summed replicas; rows = optional int32
+    device tensor of replica indices to sum instead of all)."""
+    src2, dst2 = _as2d(src), _as2d(dst)
+    _gpu(src2, dst2, rows)
+    if src2.dtype != dst2.dtype:
+        raise TypeError("replica_mean: src/dst dtype mismatch")
+    K, lds = _rows_ld(src2)
+    Ko, ldd = _rows_ld(dst2)
+    n = min(src2.shape[1], dst2.shape[1]) if n is None else int(n)
+    if n > src2.shape[1] or n > dst2.shape[1]:
+        raise ValueError("replica_mean: n exceeds the row length")
+    if rows is not None:
+        if rows.dtype != torch.int32:
+            raise TypeError("rows must be int32")
+        K = rows.numel()
+    d = float(K if divisor is None else divisor)
+    check(lib().ga_replica_mean(_dtype_code(src2), _p(src2), K, lds, _p(rows), n, d, _p(dst2), Ko, ldd,
+                                _stream()), "ga_replica_mean")
+
+
+def diloco_outer(src, master, mom, dst, n, divisor, lr, momentum, dampening, weight_decay, nesterov,
+                 first_step):
+    """Fused DiLoCo outer step over [0, n) of master/mom (see include/gym_amd.h)."""
+    src2 = _as2d(src)
+    dst2 = _as2d(dst) if dst is not None else None
+    _gpu(src2, master, mom, dst2)
+    K, lds = _rows_ld(src2)
+    Ko, ldd = _rows_ld(dst2) if dst2 is not None else (0, 0)
+    if master.numel() < n or (mom is not None and mom.numel() < n) or src2.shape[1] < n:
+        raise ValueError("diloco_outer: buffers shorter than n")
+    if dst2 is not None and dst2.shape[1] < n:
+        raise ValueError("diloco_outer: dst shorter than n")
+    master_f32 = 1 if master.dtype == torch.float32 else 0
+    if master.dtype not in (torch.float32, src2.dtype):
+        raise TypeError("diloco_outer: master must be float32 or the arena dtype")
+    if mom is not None and mom.dtype != master.dtype:
+        raise TypeError("diloco_outer: momentum dtype must match master")
+    check(lib().ga_diloco_outer(_dtype_code(src2), _p(src2), K, lds, int(n), float(divisor), _p(master), _p(mom),
+                                master_f32, int(bool(first_step)), float(lr), float(momentum), float(dampening),
+                                float(weight_decay), int(bool(nesterov)), _p(dst2), Ko, ldd, _stream()),
+          "ga_diloco_outer")
+
+
+def sparta_threshold(p):
+    return int(lib().ga_sparta_threshold(float(p)))
+
+
+def sparta_workspace(n, device):
+    nbytes = int(lib().ga_sparta_workspace_bytes(int(n)))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0):
+    """Compact the selected elements of [0, n) (mask != 0, or the Philox draw)
+    into idx (int32) and vals (= sum over the replicas of src); count[0] = number
+    selected, count[1] = overflow flag."""
+    src2 = _as2d(src)
+    _gpu(src2, idx, vals, count, work, mask)
+    K, ld = _rows_ld(src2)
+    if idx.dtype != torch.int32 or count.dtype != torch.int64 or count.numel() < 2:
+        raise TypeError("sparta_select: idx int32, count int64[2]")
+    if vals.dtype != src2.dtype or idx.numel() < cap or vals.numel() < cap:
+        raise ValueError("sparta_select: idx/vals smaller than cap")
+    if work.numel() < lib().ga_sparta_workspace_bytes(int(n)):
+        raise ValueError("sparta_select: workspace too small")
+    if mask is not None:
+        if mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n:
+            raise ValueError("sparta_select: mask must be uint8/bool with >= n elements")
+    thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
+    check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, int(n), _p(mask), int(seed) & (2**64 - 1),
+                                 int(iteration) & (2**64 - 1), thr, int(cap), _p(idx), _p(vals), _p(count),
+                                 _p(work), _stream()), "ga_sparta_select")
+
+
+def sparta_scatter(vals, idx, count, cap, divisor, dst):
+    dst2 = _as2d(dst)
+    _gpu(vals, idx, count, dst2)
+    K, ld = _rows_ld(dst2)
+    if vals.dtype != dst2.dtype:
+        raise TypeError("sparta_scatter: dtype mismatch")
+    check(lib().ga_sparta_scatter(_dtype_code(dst2), _p(vals), _p(idx), _p(count), int(cap), float(divisor),
+                                  _p(dst2), K, ld, _stream()), "ga_sparta_scatter")
+
+
+def demo_encode(plan, param, grad, delta, payload, lr, decay, wd_factor):
+    """plan: gym_amd.demo_codec.DemoPlan.  param/grad/delta: [K, ld] replica sets
+    (or 1-D); payload: int32 [K, 2*M]."""
+    p2, g2, d2, pl2 = _as2d(param), _as2d(grad), _as2d(delta), _as2d(payload)
+    _gpu(p2, g2, d2, pl2)
+    K, ld = _rows_ld(p2)
+    if g2.shape != p2.shape or d2.shape != p2.shape or g2.stride() != p2.stride() or d2.stride() != p2.stride():
+        raise ValueError("demo_encode: param/grad/delta must be replica sets of one shape")
+    if p2.shape[1] < plan.n_arena:
+        raise ValueError("demo_encode: arena shorter than the plan")
+    if pl2.dtype != torch.int32 or pl2.shape[0] != K or pl2.shape[1] < 2 * plan.M:
+        raise ValueError("demo_encode: payload must be int32 [K, >= 2*M]")
+    plan.to(p2.device)
+    check(lib().ga_demo_encode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.F), _p(plan.B),
+                               _p(p2), _p(g2), _p(d2), K, ld, float(lr), float(decay), float(wd_factor), _p(pl2),
+                               pl2.stride(0), plan.M, _stream()), "ga_demo_encode")
+
+
+def demo_decode(plan, gathered, param, grad, lr):
+    """gathered: int32 [S, >= 2*M] payloads of every node in node order;
+    param/grad: [K, ld] replica sets (grad may be None)."""
+    p2 = _as2d(param)
+    g2 = _as2d(grad) if grad is not None else None
+    ga = _as2d(gathered)
+    _gpu(p2, g2, ga)
+    K, ld = _rows_ld(p2)
+    if g2 is not None and (g2.shape != p2.shape or g2.stride() != p2.stride()):
+        raise ValueError("demo_decode: grad must match param")
+    if ga.dtype != torch.int32 or ga.shape[1] < 2 * plan.M:
+        raise ValueError("demo_decode: gathered payload must be int32 [S, >= 2*M]")
+    if p2.shape[1] < plan.n_arena:
+        raise ValueError("demo_decode: arena shorter than the plan")
+    plan.to(p2.device)
+    S = ga.shape[0]
+    check(lib().ga_demo_decode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.B), _p(ga),
+                               ga.stride(0), plan.M, S, _p(p2), _p(g2), K, ld, float(lr), _stream()),
+          "ga_demo_decode")

@@ -1,0 +1,389 @@
+"""Parity of the gfx950 kernels (through the C ABI) against the oracle and the
+reference's golden fixtures.  Bars: integer/index work bit-exact; fp32 sums
+in the same order bit-exact; reordered fp32 within 1e-6 relative; bf16 1e-2.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import demo as odemo
+from oracle import diloco as odiloco
+from oracle import reduce as oreduce
+from oracle import sparta as osparta
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from gym_amd import _lib
+    _lib.lib()
+
+
+def t(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def host(x):
+    torch.cuda.synchronize()
+    return x.float().cpu().numpy()
+
+
+# ---------------------------------------------------------------- mean --------
+@pytest.mark.parametrize("K", [1, 2, 3, 8, 32])
+@pytest.mark.parametrize("n", [4096, 1000, 12345, 1])
+def test_replica_mean_bit_exact(K, n):
+    from gym_amd import ops
+    rng = np.random.default_rng(K * 1000 + n)
+    ld = ((n + 63) // 64) * 64
+    x = rng.standard_normal((K, ld)).astype(np.float32)
+    src = t(x)
+    dst = torch.full((1, ld), 7.0, device=DEV)
+    ops.replica_mean(src, dst, n=n)
+    want = oreduce.mean_reduce(list(x[:, :n]))
+    got = host(dst)[0]
+    assert np.array_equal(got[:n], want)
+    assert (got[n:] == 7.0).all()  # nothing past n is written
+
+
+def test_replica_mean_in_place_all_replicas_and_rows():
+    from gym_amd import ops
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((5, 4160)).astype(np.float32)
+    src = t(x)
+    ops.replica_mean(src, src, n=4160)  # in place, every replica gets the mean
+    want = oreduce.mean_reduce(list(x))
+    got = host(src)
+    assert all(np.array_equal(got[k], want) for k in range(5))
+    # island subset (FedAvg islands), ascending member order
+    src = t(x)
+    rows = torch.tensor([1, 3, 4], dtype=torch.int32, device=DEV)
+    out = torch.empty(2, 4160, device=DEV)
+    ops.replica_mean(src, out, n=4160, rows=rows)
+    want = oreduce.mean_reduce(list(x), rows=[1, 3, 4])
+    assert np.array_equal(host(out)[0], want) and np.array_equal(host(out)[1], want)
+
+
+def test_replica_mean_sum_and_divisor():
+    from gym_amd import ops
+    x = np.random.default_rng(1).standard_normal((3, 640)).astype(np.float32)
+    out = torch.empty(640, device=DEV)
+    ops.replica_mean(t(x), out, divisor=1.0)
+    s = oreduce.mean_reduce(list(x), divisor=1)
+    assert np.array_equal(host(out), s)
+    ops.replica_mean(out, out, divisor=6.0)  # cross-GPU style: global divide after a sum
+    assert np.array_equal(host(out), (s / np.float32(6)).astype(np.float32))
+
+
+def test_replica_mean_bf16():
+    from gym_amd import ops
+    x = np.random.default_rng(2).standard_normal((4, 1024)).astype(np.float32)
+    src = t(x, torch.bfloat16)
+    out = torch.empty(1024, device=DEV, dtype=torch.bfloat16)
+    ops.replica_mean(src, out)
+    want = oreduce.mean_reduce(list(src.float().cpu().numpy()))
+    np.testing.assert_allclose(host(out), want, rtol=1e-2, atol=1e-2)
+
+
+def test_replica_mean_matches_reference_golden(golden):
+    from gym_amd import ops
+    z = golden("mean_reduce.npz")
+    for K in (2, 3, 8):
+        for si in range(4):
+            xs = z[f"K{K}_in_{si}"].reshape(K, -1)
+            ref = z[f"K{K}_out_{si}"].reshape(-1)
+            out = torch.empty(xs.shape[1], device=DEV)
+            ops.replica_mean(t(xs), out)
+            got = host(out)
+            if K == 2:
+                assert np.array_equal(got, ref)
+            else:
+                np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-7)
+
+
+# ---------------------------------------------------------------- DiLoCo ------
+@pytest.mark.parametrize("K,first,nesterov", [(1, True, True), (3, True, True), (3, False, True),
+                                             (8, False, False), (4, False, True)])
+def test_diloco_outer_matches_oracle(K, first, nesterov):
+    from gym_amd import ops
+    rng = np.random.default_rng(K + 10 * first)
+    n = 50_000
+    master = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    reps = (master + rng.standard_normal((K, n)) * 1e-3).astype(np.float32)
+    mom = None if first else (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    want_m, want_b, _ = odiloco.outer_step(master, mom, list(reps), lr=0.7, momentum=0.9, nesterov=nesterov)
+    g_master, g_mom = t(master), t(mom if mom is not None else np.zeros(n, np.float32))
+    src = t(reps)
+    dst = torch.empty(K, n, device=DEV)
+    ops.diloco_outer(src, g_master, g_mom, dst, n, K, 0.7, 0.9, 0.0, 0.0, nesterov, first)
+    gm, gb, gd = host(g_master), host(g_mom), host(dst)
+    np.testing.assert_allclose(gm, want_m, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(gb, want_b, rtol=0, atol=1e-6 * np.abs(master).max())
+    assert all(np.array_equal(gd[k], gm) for k in range(K))
+    # same op order as torch's SGD: all but a handful of elements bit-identical
+    assert (gm == want_m).mean() > 0.999
+
+
+def test_diloco_matches_reference_golden_chain(golden):
+    """Three outer steps of the reference's DiLoCoStrategy (K=3, H=2), replayed
+    on the GPU with the K nodes as replicas."""
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    z = golden("diloco.npz")
+    K, H, calls, ns = int(z["K"]), int(z["H"]), int(z["calls"]), int(z["nshapes"])
+    shapes = [z[f"init_{i}"].shape for i in range(ns)]
+    L = ArenaLayout(shapes)
+    master = torch.zeros(L.n, device=DEV)
+    mom = torch.zeros(L.n, device=DEV)
+    for i, v in enumerate(L.views(master)):
+        v.copy_(t(z[f"init_{i}"]))
+    reps = torch.zeros(K, L.n, device=DEV)
+    first = True
+    for call in range(calls):
+        if not odiloco.is_outer_step(call, H):
+            continue
+        for k in range(K):
+            for i, v in enumerate(L.views(reps[k])):
+                v.copy_(t(z[f"before_{call}_{i}"][k]))
+        ops.diloco_outer(reps, master, mom, reps, L.n, K, 0.7, 0.9, 0.0, 0.0, True, first)
+        first = False
+        for i in range(ns):
+            ref_m = z[f"master_{call}_{i}"]
+            np.testing.assert_allclose(host(L.views(master)[i]), ref_m, rtol=1e-6, atol=1e-8)
+            for k in range(K):
+                np.testing.assert_allclose(host(L.views(reps[k])[i]), z[f"after_{call}_{i}"][k], rtol=1e-6,
+                                           atol=1e-8)
+        # continue from the reference's own state (as the oracle test does)
+        for i, v in enumerate(L.views(master)):
+            v.copy_(t(z[f"master_{call}_{i}"]))
+        for i, v in enumerate(L.views(mom)):
+            v.copy_(t(z[f"mom_{call}_{i}"]))
+
+
+def test_diloco_bf16_params_fp32_master():
+    from gym_amd import ops
+    rng = np.random.default_rng(9)
+    n, K = 8192, 4
+    master = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    reps = (master + rng.standard_normal((K, n)) * 1e-2).astype(np.float32)
+    src = t(reps, torch.bfloat16)
+    want_m, _, _ = odiloco.outer_step(master, None, list(src.float().cpu().numpy()))
+    gm, gb = t(master), torch.zeros(n, device=DEV)
+    ops.diloco_outer(src, gm, gb, src, n, K, 0.7, 0.9, 0.0, 0.0, True, True)
+    np.testing.assert_allclose(host(gm), want_m, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(host(src)[0], want_m, rtol=1e-2, atol=1e-3)
+
+
+# ---------------------------------------------------------------- SPARTA ------
+def _sparta_buffers(n, cap):
+    from gym_amd import ops
+    return (torch.empty(cap, dtype=torch.int32, device=DEV), torch.zeros(2, dtype=torch.int64, device=DEV),
+            ops.sparta_workspace(n, DEV))
+
+
+@pytest.mark.parametrize("n,p,K", [(1_000_003, 0.005, 1), (65_536, 0.3, 3), (4095, 0.5, 2), (5, 0.9, 1)])
+def test_sparta_philox_select_gather_scatter(n, p, K):
+    from gym_amd import ops
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    seed, it = 0x1234_5678_9ABC, 17
+    mask = osparta.philox_mask(n, seed, it, p)
+    want_idx = np.flatnonzero(mask)
+    cap = len(want_idx) + 64
+    idx, count, work = _sparta_buffers(n, cap)
+    vals = torch.empty(cap, device=DEV)
+    src = t(x)
+    ops.sparta_select(src, n, cap, idx, vals, count, work, seed=seed, iteration=it, p=p)
+    c = host(count).astype(np.int64)
+    assert c[0] == len(want_idx) and c[1] == 0
+    assert np.array_equal(idx.cpu().numpy()[: c[0]], want_idx)
+    assert np.array_equal(host(vals)[: c[0]], oreduce.mean_reduce(list(x[:, want_idx]), divisor=1))
+    ops.sparta_scatter(vals, idx, count, cap, float(K), src)
+    want = osparta.sparse_average(list(x), mask)
+    got = host(src)
+    for k in range(K):
+        assert np.array_equal(got[k], want[k])
+
+
+def test_sparta_overflow_flag():
+    from gym_amd import ops
+    n = 10_000
+    x = t(np.ones((1, n), np.float32))
+    idx, count, work = _sparta_buffers(n, 100)
+    vals = torch.empty(100, device=DEV)
+    ops.sparta_select(x, n, 100, idx, vals, count, work, seed=1, iteration=0, p=0.5)
+    c = count.cpu().numpy()
+    assert c[0] > 100 and c[1] == 1
+    ops.sparta_scatter(vals, idx, count, 100, 1.0, x)  # writes only the first cap entries
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_sparta_mask_mode_matches_reference_golden(golden, K):
+    """The reference's own masks (rank 0's, logged) through the mask-mode
+    kernels, the K nodes as replicas: identical to SPARTAStrategy's result."""
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    z = golden("sparta.npz")
+    calls, ns = int(z["calls"]), int(z["nshapes"])
+    shapes = [z[f"K{K}_before_0_{i}"].shape[1:] for i in range(ns)]
+    L = ArenaLayout(shapes)
+    for call in range(calls):
+        reps = torch.zeros(K, L.n, device=DEV)
+        mask = torch.zeros(L.n, dtype=torch.uint8, device=DEV)
+        for i in range(ns):
+            n_i = int(np.prod(shapes[i]))
+            m = np.unpackbits(z[f"K{K}_mask_{call}_{i}"])[:n_i].astype(np.uint8)
+            L.views(mask)[i].copy_(torch.from_numpy(m.reshape(shapes[i])))
+            for k in range(K):
+                L.views(reps[k])[i].copy_(t(z[f"K{K}_before_{call}_{i}"][k]))
+        cap = int(mask.sum().item())
+        idx, count, work = _sparta_buffers(L.n, cap)
+        vals = torch.empty(cap, device=DEV)
+        ops.sparta_select(reps, L.n, cap, idx, vals, count, work, mask=mask)
+        ops.sparta_scatter(vals, idx, count, cap, float(K), reps)
+        for i in range(ns):
+            for k in range(K):
+                got = host(L.views(reps[k])[i])
+                ref = z[f"K{K}_after_{call}_{i}"][k]
+                if K == 2:
+                    assert np.array_equal(got, ref)
+                else:
+                    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-9)
+
+
+# ---------------------------------------------------------------- DeMo --------
+DEMO_SHAPES = [(128, 128), (66, 128), (768,), (8, 4, 3, 3), (10,), (58, 29), (64, 64)]
+
+
+def _demo_setup(shapes, K, seed=0, dtype=torch.float32):
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    L = ArenaLayout(shapes)
+    plan = DemoPlan(L, chunk=64, topk=32)
+    rng = np.random.default_rng(seed)
+    arrs = {}
+    for name in ("p", "g", "d"):
+        host_arr = np.zeros((K, L.n), np.float32)
+        for k in range(K):
+            for o, nel in zip(L.offsets, L.numels):
+                host_arr[k, o:o + nel] = rng.standard_normal(nel) * (0.02 if name == "p" else 1e-2)
+        if name == "p":
+            host_arr[:] = host_arr[0]  # DeMo keeps params identical across nodes
+        arrs[name] = host_arr
+    return L, plan, arrs
+
+
+def _payload_host(pl, plan):
+    a = pl.cpu().numpy()
+    return a[:, : plan.M], a[:, plan.M: 2 * plan.M].view(np.float32)
+
+
+@pytest.mark.parametrize("K", [1, 2, 3])
+def test_demo_encode_decode_matches_oracle(K):
+    from gym_amd import ops
+    shapes = DEMO_SHAPES
+    L, plan, a = _demo_setup(shapes, K, seed=K)
+    lr, decay, wd = 0.01, 0.999, 0.1
+    wdf = float(np.float32(1.0 - lr * wd))
+    P, G, D = t(a["p"]), t(a["g"]), t(a["d"])
+    payload = torch.zeros(K, 2 * plan.M, dtype=torch.int32, device=DEV)
+    ops.demo_encode(plan, P, G, D, payload, lr, decay, wdf)
+    gidx, gval = _payload_host(payload, plan)
+    grad_out = torch.zeros_like(G)
+    ops.demo_decode(plan, payload, P, grad_out, lr)
+    gP, gD, gS = host(P), host(D), host(grad_out)
+    for ti, (shape, off, nel) in enumerate(zip(L.shapes, L.offsets, L.numels)):
+        R, C, n1, n2 = odemo.tensor_view(shape, 64)
+        p0 = a["p"][0, off:off + nel].reshape(shape)
+        deltas = [a["d"][k, off:off + nel].reshape(shape) for k in range(K)]
+        grads = [a["g"][k, off:off + nel].reshape(shape) for k in range(K)]
+        want_p, want_d, want_s, sent = odemo.demo_step(p0, deltas, grads, lr, decay, 32, 64, wd)
+        e0 = sum(plan.entries_per_tensor[:ti])
+        ne = plan.entries_per_tensor[ti]
+        kk = max(1, min(32, n1 * n2))
+        for k in range(K):
+            idx_k = gidx[k, e0:e0 + ne].reshape(R // n1, C // n2, kk)
+            val_k = gval[k, e0:e0 + ne].reshape(R // n1, C // n2, kk)
+            oidx, oval = sent[k]
+            # index sets exact where the k-th magnitude is not (nearly) tied
+            d64 = np.asarray(deltas[k], np.float64) * decay + lr * np.asarray(grads[k], np.float64)
+            margin = odemo.kth_margin(odemo.encode(d64, shape, 64), 32).reshape(R // n1, C // n2)
+            scale = np.abs(oval).max()
+            for y in range(R // n1):
+                for x in range(C // n2):
+                    if margin[y, x] > 1e-5 * scale:
+                        assert np.array_equal(idx_k[y, x], oidx[y, x]), (shape, y, x)
+                        np.testing.assert_allclose(val_k[y, x], oval[y, x], rtol=0, atol=1e-5 * scale)
+            # residual compared in the chunks whose selected set is unambiguous
+            okc = margin > 1e-5 * scale
+            okel = np.repeat(np.repeat(okc, n1, axis=0), n2, axis=1).reshape(shape)
+            np.testing.assert_allclose(gD[k, off:off + nel].reshape(shape)[okel], want_d[k][okel], rtol=0,
+                                       atol=1e-5 * max(np.abs(d64).max(), 1e-12))
+        # sign-SGD apply: signs agree except where the decoded value is ~0
+        s = gS[0, off:off + nel].reshape(shape)
+        assert (s == want_s).mean() > 0.995
+        ok = s == want_s
+        np.testing.assert_allclose(gP[0, off:off + nel].reshape(shape)[ok], want_p[ok], rtol=0, atol=1e-6)
+        for k in range(1, K):
+            assert np.array_equal(gP[k, off:off + nel], gP[0, off:off + nel])
+    # padding between tensors stays exactly zero in every arena
+    for arr in (gP, gD, gS):
+        for o, nel, o2 in zip(L.offsets, L.numels, L.offsets[1:] + [L.n]):
+            assert (arr[:, o + nel:o2] == 0).all()
+
+
+def test_demo_matches_reference_golden_steps(golden):
+    """Three DeMo.step()s of the reference (K=2 nodes over gloo) replayed with
+    the 2 nodes as replicas."""
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    z = golden("demo_steps.npz")
+    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
+    lr, wd, decay = float(z["lr"]), float(z["wd"]), float(z["decay"])
+    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
+    L = ArenaLayout(shapes)
+    plan = DemoPlan(L, chunk=int(z["chunk"]), topk=int(z["topk"]))
+    assert plan.reference_bytes() == int(z["tx_0"])
+    P = torch.zeros(K, L.n, device=DEV)
+    D = torch.zeros(K, L.n, device=DEV)
+    G = torch.zeros(K, L.n, device=DEV)
+    payload = torch.zeros(K, 2 * plan.M, dtype=torch.int32, device=DEV)
+    wdf = float(np.float32(1.0 - lr * wd))
+    for step in range(steps):
+        for i in range(ns):  # start each step from the reference state
+            for k in range(K):
+                L.views(P[k])[i].copy_(t(z[f"p_before_{step}_{i}"]))
+                L.views(D[k])[i].copy_(t(z[f"delta_before_{step}_{i}"][k]))
+                L.views(G[k])[i].copy_(t(z[f"grad_{step}_{i}"][k]))
+        ops.demo_encode(plan, P, G, D, payload, lr, decay, wdf)
+        ops.demo_decode(plan, payload, P, G, lr)
+        for i in range(ns):
+            ref_s = z[f"sign_{step}_{i}"]
+            s = host(L.views(G[0])[i])
+            assert (s == ref_s).mean() > 0.995
+            ok = s == ref_s
+            np.testing.assert_allclose(host(L.views(P[0])[i])[ok], z[f"p_after_{step}_{i}"][ok], rtol=0, atol=1e-6)
+            for k in range(K):
+                ref_d = z[f"delta_after_{step}_{i}"][k]
+                scale = max(np.abs(ref_d).max(), lr * np.abs(z[f"grad_{step}_{i}"][k]).max())
+                np.testing.assert_allclose(host(L.views(D[k])[i]), ref_d, rtol=0, atol=2e-5 * scale)
+
+
+def test_demo_all_zero_chunk_tie_rule():
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    L = ArenaLayout([(128, 128)])
+    plan = DemoPlan(L)
+    P = torch.zeros(1, L.n, device=DEV)
+    payload = torch.full((1, 2 * plan.M), -1, dtype=torch.int32, device=DEV)
+    ops.demo_encode(plan, P, P.clone(), P.clone(), payload, 0.01, 0.999, 1.0)
+    idx, val = _payload_host(payload, plan)
+    assert (val == 0).all()
+    assert all(np.array_equal(idx[0, c * 32:(c + 1) * 32], np.arange(32)) for c in range(4))
