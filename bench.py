@@ -1,0 +1,324 @@
+"""Strategy-communication-step benchmark (BASELINE.json metric: strategy-step
+param GB/s (%HBM/xGMI peak) + ms/outer step, GPT-2 124M, 1-8 GPUs).
+
+Headline workload (configs[2]): the DiLoCo outer step of GPT-2 124M over 8
+simulated nodes per GPU (batched-replica arena [8, N] per GPU; at N GPUs the
+nodes of all GPUs are averaged: in-kernel over the local 8, RCCL across GPUs;
+weak scaling).  One timed "step" = one outer step: sum/average of every
+node's parameters, pseudo-gradient, outer Nesterov SGD, write-back into every
+node.  Inputs are synthetic, resident in HBM before timing starts.
+
+value = node-parameter bytes averaged per second over the whole job
+        = K_total * 4 * N_params / t_step  ("param GB/s"); ms_per_step = t_step.
+roofline = the fused ga_diloco_outer kernel: algorithmic HBM bytes per launch
+        ((2*K_local + 4) * 4 * n: read every replica, master, momentum; write
+        them back) / its HIP-event-timed duration, against 8 TB/s.
+cpu_baseline = the numpy oracle's outer step (oracle/diloco.py) on rank 0, on a
+        bounded slice of the same arena, single thread.
+
+Extra lines in "extras" (same timing rules, not the headline): SPARTA (K=32
+replicas per GPU, p=0.005, Philox mask), SimpleReduce (char-level nanoGPT,
+8 replicas per GPU), DeMo (GPT-2 350M, one node per GPU, chunk 64 / top-k 32).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-extras]
+       torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from gym_amd import ops  # noqa: E402
+from gym_amd.arena import ArenaLayout, ReplicaSet  # noqa: E402
+from gym_amd.comm import Collective  # noqa: E402
+from gym_amd.engine import DeMoCodec, DiLoCoOuter, MeanReduce, Sparta  # noqa: E402
+from gym_amd.shapes import MODELS, numel  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md
+MFMA_F32_TFLOPS = 157.3    # dense fp32 MFMA (= f32 vector) peak
+XGMI_LINK_GBS = 153.0      # per xGMI link (SURVEY §8(d) roofline model)
+
+
+def setup_dist(gpus):
+    if gpus > 1 or "RANK" in os.environ:
+        local = int(os.environ.get("LOCAL_RANK", 0))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    return Collective()
+
+
+def synth_replicas(layout, K, rank, dev, dtype=torch.float32):
+    """Node k: shared start N(0, 0.02) (seed 1234) + drift N(0, 1e-3) (seed 1000+k),
+    the layout's padding kept at zero (SURVEY §8(d) synthetic inputs)."""
+    rs = ReplicaSet(layout, K, dev, dtype)
+    g = torch.Generator(device=dev)
+    base = torch.empty(layout.n, device=dev)
+    g.manual_seed(1234)
+    base.normal_(0.0, 0.02, generator=g)
+    pad = torch.ones(layout.n, device=dev, dtype=torch.bool)
+    for o, n in zip(layout.offsets, layout.numels):
+        pad[o:o + n] = False
+    base[pad] = 0
+    for k in range(K):
+        g.manual_seed(1000 + rank * K + k)
+        rs.data[k].normal_(0.0, 1e-3, generator=g)
+        rs.data[k].add_(base)
+        rs.data[k][pad] = 0
+    return rs
+
+
+def timed_loop(fn, steps, warmup, coll):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if coll.world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if coll.world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if coll.world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt / steps
+
+
+class KernelTimer:
+    """HIP events around one kernel launch, on the stream it is launched on."""
+
+    def __init__(self):
+        self.pairs = []
+        self.on = False
+
+    def wrap(self, fn):
+        def timed(*a, **kw):
+            if not self.on:
+                return fn(*a, **kw)
+            s = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            r = fn(*a, **kw)
+            e1.record(s)
+            self.pairs.append((e0, e1))
+            return r
+        return timed
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else None
+
+
+def cpu_baseline_diloco(n_total, K, budget_s=12.0):
+    """Oracle outer step on a slice of the arena (rank 0, one host thread)."""
+    sys.path.insert(0, ROOT)
+    from oracle import diloco as odiloco
+    n = min(n_total, 8 * 1024 * 1024)
+    rng = np.random.default_rng(0)
+    master = (rng.standard_normal(n, dtype=np.float32) * 0.02).astype(np.float32)
+    reps = [(master + rng.standard_normal(n, dtype=np.float32) * 1e-3).astype(np.float32) for _ in range(K)]
+    mom = np.zeros(n, np.float32)
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while time.perf_counter() < t_end or len(times) < 2:
+        t0 = time.perf_counter()
+        m2, b2, _ = odiloco.outer_step(master, mom, reps)
+        reps = [m2] * K  # write-back into every node, as the step does
+        times.append(time.perf_counter() - t0)
+        if len(times) >= 50:
+            break
+    t = float(np.median(times))
+    return {"value": round(K * 4 * n / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/diloco.outer_step, K={K} nodes x {n} fp32 elements (first {n} of the "
+                      f"{n_total}-element arena), median of {len(times)} steps, {t * 1e3:.1f} ms/step; "
+                      f"scaled per node-parameter byte"}
+
+
+def bench_diloco(args, coll, dev):
+    shapes = MODELS[args.model]()
+    layout = ArenaLayout(shapes)
+    n = layout.padded_to(coll.world)
+    layout.n = n
+    K = args.replicas
+    rs = synth_replicas(layout, K, coll.rank, dev)
+    eng = DiLoCoOuter(coll, K, n, dev, torch.float32)
+    eng.init_master(rs.data[0])
+    timer = KernelTimer()
+    eng._outer = timer.wrap(eng._outer)
+    reps = rs.data
+    eng(reps)  # first outer step (momentum buffer created); timed steps use the warm buffer
+    timer.on = True
+    t = timed_loop(lambda: eng(reps), args.steps, args.warmup, coll)
+    kern_ms = timer.mean_ms()
+    K_total = K * coll.world
+    n_params = numel(shapes)
+    value = K_total * 4 * n_params / t / 1e9
+    per = eng.per
+    if coll.world == 1:  # read every replica, master, mom; write master, mom, every replica
+        alg_bytes = (2 * K + 4) * per * 4
+    else:  # sharded: read the reduce-scattered sum shard, master, mom; write master, mom, param shard
+        alg_bytes = 6 * per * 4
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    out = {
+        "ms_per_step": t * 1e3, "value": value, "K_total": K_total, "n_params": n_params,
+        "kernel_ms": kern_ms, "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "ga_diloco_outer", "bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4)},
+    }
+    if coll.world > 1:
+        S = 4 * n
+        busbw = 2 * (coll.world - 1) / coll.world * S / t / 1e9  # whole step, kernels included
+        out["xgmi"] = {"collective": "reduce_scatter+all_gather (= all-reduce bytes)", "bytes": S,
+                       "bus_GBps_whole_step": round(busbw, 1),
+                       "frac_per_link_ring": round(busbw / XGMI_LINK_GBS, 3),
+                       "frac_7link": round(busbw / (7 * XGMI_LINK_GBS), 3)}
+    return out
+
+
+def bench_sparta(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
+    shapes = MODELS[model]()
+    layout = ArenaLayout(shapes)
+    rs = synth_replicas(layout, K, coll.rank, dev)
+    eng = Sparta(coll, K, layout.n, dev, torch.float32, p)
+    it = [0]
+
+    def step():
+        eng(rs.data, seed=42, iteration=it[0])
+        it[0] += 1
+
+    t = timed_loop(step, args.steps, args.warmup, coll)
+    eng.check()
+    M = int(eng.count[0].item())
+    alg = 2 * 4 * K * M + 4 * M * 2  # gather K replicas + scatter K replicas + idx write/read
+    return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
+            "K_local": K, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1)}
+
+
+def bench_simple(args, coll, dev, K=8, model="gpt2-char"):
+    shapes = MODELS[model]()
+    layout = ArenaLayout(shapes)
+    layout.n = layout.padded_to(coll.world)
+    rs = synth_replicas(layout, K, coll.rank, dev)
+    eng = MeanReduce(coll, K, layout.n, dev, torch.float32)
+    t = timed_loop(lambda: eng(rs.data), args.steps, args.warmup, coll)
+    return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
+            "K_local": K, "model": model}
+
+
+def bench_demo(args, coll, dev, model="gpt2-350m"):
+    shapes = MODELS[model]()
+    layout = ArenaLayout(shapes)
+    P = synth_replicas(layout, 1, 0, dev).data  # identical params on every node
+    G = synth_replicas(layout, 1, coll.rank + 7, dev).data
+    D = torch.zeros_like(P)
+    codec = DeMoCodec(coll, 1, layout, dev)
+    te, td = KernelTimer(), KernelTimer()
+    codec.encode = te.wrap(codec.encode)
+    codec.decode = td.wrap(codec.decode)
+    te.on = td.on = True
+    t = timed_loop(lambda: codec(P, G, D, 1e-3, 0.999, 0.0), args.steps, args.warmup, coll)
+    plan = codec.plan
+    flops_one = 0
+    for s in shapes:
+        from gym_amd.demo_codec import codec_view
+        R, C, n1, n2 = codec_view(s, 64)
+        flops_one += 2 * (R // n1) * (C // n2) * 2 * 64 ** 3  # two zero-padded 64^3 products per transform
+    enc_ms, dec_ms = te.mean_ms(), td.mean_ms()
+    return {"ms_per_step": round(t * 1e3, 4), "model": model, "nodes": coll.world,
+            "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+            "encode_TFLOPs": round(2 * flops_one / (enc_ms * 1e-3) / 1e12, 2),
+            "decode_TFLOPs": round(flops_one / (dec_ms * 1e-3) / 1e12, 2),
+            "mfma_f32_peak_TFLOPs": MFMA_F32_TFLOPS, "payload_entries": plan.M,
+            "ref_bytes_tx": plan.reference_bytes()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="gpt2-124m")
+    ap.add_argument("--replicas", type=int, default=8, help="simulated nodes per GPU")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--only", default=None, help="diloco|sparta|simple|demo (profiling runs)")
+    args = ap.parse_args()
+
+    coll = setup_dist(args.gpus)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.backends.cuda.matmul.allow_tf32 = False
+
+    if args.only and args.only != "diloco":
+        fn = {"sparta": bench_sparta, "simple": bench_simple, "demo": bench_demo}[args.only]
+        r = fn(args, coll, dev)
+        if coll.rank == 0:
+            print(json.dumps({"only": args.only, **r}), flush=True)
+        return
+
+    head = bench_diloco(args, coll, dev)
+    extras = {}
+    if not args.no_extras:
+        for name, fn in (("sparta_k32", bench_sparta), ("simple_reduce_char_k8", bench_simple),
+                         ("demo_350m", bench_demo)):
+            torch.cuda.empty_cache()
+            try:
+                extras[name] = fn(args, coll, dev)
+            except Exception as e:  # keep the headline line even if an extra fails
+                extras[name] = {"error": repr(e)[:300]}
+    if coll.rank != 0:
+        if coll.world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline_diloco(head["n_params"], args.replicas)
+    K_total = head["K_total"]
+    line = {
+        "metric": "strategy-step param GB/s (%HBM/xGMI peak) + ms/outer step, GPT-2 124M, 1-8 GPUs",
+        "value": round(head["value"], 2),
+        "unit": "GB/s",
+        "n_gpus": coll.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(head["ms_per_step"], 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (GPT-2 124M parameter shapes, N(0,0.02) start + per-node N(0,1e-3) drift)",
+        "config": {"workload": f"DiLoCo outer step (configs[2]), {args.model}, {args.replicas} simulated nodes "
+                               f"per GPU as a batched-replica arena, {K_total} nodes total; fused "
+                               f"average+pseudo-grad+Nesterov SGD(lr=0.7, mu=0.9) + RCCL reduce-scatter/all-gather "
+                               f"across GPUs",
+                   "model": args.model, "nodes_per_gpu": args.replicas, "nodes_total": K_total,
+                   "n_params": head["n_params"], "parallelism": f"dp{K_total} (simulated nodes)"},
+        "roofline": head["roofline"],
+        "cpu_baseline": cpu,
+    }
+    if "xgmi" in head:
+        line["xgmi"] = head["xgmi"]
+    if extras:
+        line["extras"] = extras
+    print(json.dumps(line), flush=True)
+    if coll.world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

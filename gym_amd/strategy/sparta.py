@@ -1,0 +1,174 @@
+"""SPARTA: after every inner step, average a random sparse subset of the
+parameters across nodes.
+
+API of exogym/strategy/sparta.py:14-282: SparseCommunicator(index_selector),
+SPARTAStrategy(inner_optim=None, p_sparta=0.005, **kwargs), IndexSelector,
+RandomIndexSelector, ShuffledSequentialIndexSelector, PartitionedIndexSelector.
+
+The reference loops over every tensor: draw a Bernoulli(p) mask, broadcast the
+bool mask from rank 0, gather, all-reduce, divide, masked_scatter.  Here one
+select+gather kernel runs over the whole arena, ONE all-reduce moves the
+packed values (about p*N elements), one scatter kernel writes them back.
+
+Mask sources (RandomIndexSelector(mask_source=...)):
+  "philox" (default) — each element's Bernoulli(p) draw comes from
+      Philox4x32-10 keyed by a per-run seed (rank 0's torch.initial_seed(),
+      broadcast once) and the iteration; every rank computes the identical mask
+      in-kernel, so the reference's per-step N-byte mask broadcast disappears.
+      Same distribution as the reference, a different random stream.
+  "torch" — the reference's exact draw, torch.bernoulli(torch.full(shape, p))
+      per tensor on the device in parameter order, rank 0's mask broadcast;
+      bit-identical selections to the reference given the same generator state.
+The ShuffledSequential / Partitioned selectors are the reference's algorithms
+(torch draws on the device) feeding the mask-mode kernels.
+"""
+import math
+from typing import Optional, Union
+
+import torch
+
+from ..engine import Sparta
+from .communicate_optimize_strategy import CommunicateOptimizeStrategy, CommunicationModule
+from .optim import OptimSpec
+
+
+class IndexSelector:
+    def __init__(self, p):
+        self.state = {}
+        self.p = p
+
+    def get_indices(self, param, iteration):
+        return torch.ones_like(param, dtype=torch.bool)
+
+
+class RandomIndexSelector(IndexSelector):
+    def __init__(self, p, mask_source="philox"):
+        super().__init__(p)
+        if mask_source not in ("philox", "torch"):
+            raise ValueError(f"mask_source must be 'philox' or 'torch', got {mask_source!r}")
+        self.mask_source = mask_source
+
+    def get_indices(self, param, iteration):
+        return torch.bernoulli(torch.full(param.shape, self.p, device=param.device)).bool()
+
+
+class ShuffledSequentialIndexSelector(IndexSelector):
+    """Cycles through a per-tensor random permutation in ceil(1/p) chunks."""
+
+    def get_indices(self, param, iteration):
+        n = param.numel()
+        if n == 0:
+            return torch.zeros_like(param, dtype=torch.bool)
+        st = self.state.get(param)
+        if st is None:
+            st = self.state[param] = {"num_partitions": max(1, math.ceil(1.0 / self.p)),
+                                      "shuffled_indices": torch.randperm(n, device=param.device)}
+        parts = st["num_partitions"]
+        c = iteration % parts
+        size, rem = divmod(n, parts)
+        lo = c * size + min(c, rem)
+        hi = lo + size + (1 if c < rem else 0)
+        mask = torch.zeros(n, dtype=torch.bool, device=param.device)
+        sel = st["shuffled_indices"][lo:hi]
+        if sel.numel() > 0:
+            mask[sel] = True
+        return mask.view(param.shape)
+
+
+class PartitionedIndexSelector(IndexSelector):
+    """Random partition of each tensor into ceil(1/p) parts, visited in turn,
+    re-drawn when a cycle ends."""
+
+    def _set_partition(self, param):
+        st = self.state[param]
+        st["curr_partition"] = 0
+        parts = max(1, min(math.ceil(1.0 / self.p), param.numel()))
+        st["num_partitions"] = parts
+        if param.numel() > 0:
+            st["partitions"] = torch.rand(param.numel(), device=param.device).argsort() % parts
+        else:
+            st["partitions"] = torch.empty(0, dtype=torch.long, device=param.device)
+
+    def get_indices(self, param, iteration):
+        if param.numel() == 0:
+            return torch.zeros_like(param, dtype=torch.bool)
+        if param not in self.state:
+            self.state[param] = {}
+            self._set_partition(param)
+        elif self.state[param]["curr_partition"] >= self.state[param]["num_partitions"]:
+            self._set_partition(param)
+        st = self.state[param]
+        if st["num_partitions"] == 0:
+            return torch.zeros_like(param, dtype=torch.bool)
+        mask = (st["partitions"] == st["curr_partition"]).view(param.shape).bool()
+        st["curr_partition"] += 1
+        return mask
+
+
+class SparseCommunicator(CommunicationModule):
+    def __init__(self, index_selector, **kwargs):
+        super().__init__(**kwargs)
+        self.index_selector = index_selector
+        self.iteration = 0
+        self._engine = None
+        self._seed = None
+        self._mask = None
+
+    def _init_node(self, model, rank, num_nodes):
+        pass
+
+    def _setup(self):
+        s = self.strategy
+        a = s.arena
+        self._engine = Sparta(s.coll, 1, a.n, a.device, a.dtype, self.index_selector.p)
+
+    def _philox_mode(self):
+        sel = self.index_selector
+        return isinstance(sel, RandomIndexSelector) and sel.mask_source == "philox"
+
+    def _shared_seed(self):
+        if self._seed is None:
+            s = self.strategy
+            t = torch.tensor([torch.initial_seed() & (2**63 - 1)], dtype=torch.int64, device=s.arena.device)
+            s.coll.broadcast_(t, 0)
+            self._seed = int(t.item())
+        return self._seed
+
+    def _build_mask(self, model):
+        """Reference mask path: per-tensor selector draws into one uint8 mask
+        arena (frozen / grad-less tensors stay 0), then rank 0's is broadcast."""
+        s = self.strategy
+        a = s.arena
+        if self._mask is None:
+            self._mask = torch.zeros(a.n, dtype=torch.uint8, device=a.device)
+        views = a.layout.views(self._mask)
+        for p, v in zip(a.params, views):
+            if not p.requires_grad or p.grad is None:
+                v.zero_()
+                continue
+            v.copy_(self.index_selector.get_indices(p, self.iteration))
+        s.coll.broadcast_(self._mask, 0)
+        return self._mask
+
+    def communicate(self, model, rank: int, num_nodes: int, local_step: int) -> None:
+        if num_nodes > 1:
+            if self._engine is None:
+                self._setup()
+            s = self.strategy
+            s.arena.check_bound()
+            with torch.no_grad():
+                reps = s.arena.flat.view(1, -1)
+                if self._philox_mode():
+                    self._engine(reps, seed=self._shared_seed(), iteration=self.iteration)
+                else:
+                    self._engine(reps, mask=self._build_mask(model))
+        self.iteration += 1
+
+
+class SPARTAStrategy(CommunicateOptimizeStrategy):
+    def __init__(self, inner_optim: Optional[Union[str, OptimSpec]] = None, p_sparta=0.005,
+                 mask_source="philox", **kwargs):
+        index_selector = RandomIndexSelector(p_sparta, mask_source=mask_source)
+        sparse_comm = SparseCommunicator(index_selector)
+        super().__init__(inner_optim=inner_optim, communication_modules=[sparse_comm], **kwargs)
+        self.index_selector = index_selector
