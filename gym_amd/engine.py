@@ -130,7 +130,7 @@ class Sparta:
     def __init__(self, coll: Collective, K_local, n, device, dtype, p):
         self.coll, self.K_local, self.n, self.p = coll, int(K_local), int(n), float(p)
         self.K_total = coll.world * self.K_local
-        self.device, self.dtype = device, dtype
+        self.device, self.dtype = torch.device(device), dtype
         self.cap = sparta_capacity(n, self.p)
         self.idx = torch.empty(self.cap, dtype=torch.int32, device=device)
         self.vals = torch.empty(self.cap, dtype=dtype, device=device)
@@ -165,10 +165,13 @@ class Sparta:
                           iteration=iteration, p=self.p)
         self.coll.all_reduce_(self.vals[:cap_used])
         ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps)
-        if mask is None:
+        if mask is None:  # overflow flag read back asynchronously, checked next step
             self._flag_host.copy_(self.count, non_blocking=True)
-            self._flag_event = torch.cuda.Event()
-            self._flag_event.record()
+            if self.device.type == "cuda":
+                self._flag_event = torch.cuda.Event()
+                self._flag_event.record()
+            elif int(self._flag_host[1]) != 0:
+                raise RuntimeError(f"SPARTA: {int(self._flag_host[0])} elements selected > capacity {self.cap}")
 
 
 class DeMoCodec:

@@ -1,0 +1,103 @@
+"""Assertions shared by the CPU (oracle stand-in) and GPU (real kernel) runs of
+tests/strategy_scenarios.py: every rank's final state against the reference's
+golden fixtures or the oracle."""
+import os
+import random
+
+import numpy as np
+
+from oracle import demo as odemo
+from oracle import reduce as oreduce
+from oracle import sparta as osparta
+
+
+def check_simple(res, world, golden_dir):
+    z = np.load(os.path.join(golden_dir, "mean_reduce.npz"))
+    for r in range(world):
+        for si in range(4):
+            got, ref = res[r][f"grad_{si}"], z[f"K{world}_out_{si}"]
+            if world == 2:
+                assert np.array_equal(got, ref)
+            else:
+                np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-7)
+
+
+def check_diloco(res, world, golden_dir):
+    z = np.load(os.path.join(golden_dir, "diloco.npz"))
+    ns, calls = int(z["nshapes"]), int(z["calls"])
+    for call in range(calls):
+        for i in range(ns):
+            for r in range(world):
+                # no chaining here: three outer steps run end to end on our state
+                np.testing.assert_allclose(res[r][f"after_{call}_{i}"], z[f"after_{call}_{i}"][r], rtol=2e-6,
+                                           atol=2e-8)
+
+
+def check_sparta(res, world, golden_dir):
+    z = np.load(os.path.join(golden_dir, "sparta.npz"))
+    ns, calls = int(z["nshapes"]), int(z["calls"])
+    for call in range(calls):
+        for i in range(ns):
+            for r in range(world):
+                got, ref = res[r][f"after_{call}_{i}"], z[f"K{world}_after_{call}_{i}"][r]
+                if world == 2:
+                    assert np.array_equal(got, ref)
+                else:
+                    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-9)
+
+
+def check_sparta_philox(res, world, golden_dir):
+    seed = int(res[0]["seed"])
+    n = int(res[0]["n"])
+    assert all(int(res[r]["seed"]) == seed for r in range(world))  # rank 0's seed everywhere
+    reps = [res[r]["before"] for r in range(world)]
+    for it in (0, 1):
+        reps = osparta.sparse_average(reps, osparta.philox_mask(n, seed, it, 0.05))
+    for r in range(world):
+        np.testing.assert_array_equal(res[r]["after"], reps[r]) if world == 2 else \
+            np.testing.assert_allclose(res[r]["after"], reps[r], rtol=1e-6, atol=1e-9)
+
+
+def check_fedavg(res, world, golden_dir, island_size=None):
+    nt = 3
+    before = [[res[r][f"before_{i}"] for i in range(nt)] for r in range(world)]
+    for r in range(world):
+        for i in range(nt):
+            assert np.array_equal(res[r][f"after0_{i}"], before[r][i])  # local_step 0: no averaging
+    if island_size is None or island_size >= world:
+        islands = [set(range(world))]
+    else:
+        rng = random.Random(1234)
+        ranks = list(range(world))
+        rng.shuffle(ranks)
+        islands = [set(ranks[j:j + island_size]) for j in range(0, world, island_size)]
+    for r in range(world):
+        isl = next(s for s in islands if r in s)
+        for i in range(nt):
+            want = oreduce.mean_reduce([before[m][i] for m in sorted(isl)])
+            np.testing.assert_allclose(res[r][f"after1_{i}"], want, rtol=1e-6, atol=1e-9)
+
+
+def check_demo(res, world, golden_dir):
+    z = np.load(os.path.join(golden_dir, "demo_steps.npz"))
+    ns, steps = int(z["nshapes"]), int(z["steps"])
+    lr = float(z["lr"])
+    for step in range(steps):
+        assert int(res[0][f"tx_{step}"]) == int(z[f"tx_{step}"])
+        assert int(res[0][f"rx_{step}"]) == int(z[f"rx_{step}"])
+        for i in range(ns):
+            ref_s = z[f"sign_{step}_{i}"]
+            for r in range(world):
+                s = res[r][f"sign_{step}_{i}"]
+                assert (s == ref_s).mean() > 0.995
+                ok = s == ref_s
+                np.testing.assert_allclose(res[r][f"p_{step}_{i}"][ok], z[f"p_after_{step}_{i}"][ok], rtol=0,
+                                           atol=1e-6)
+                assert np.array_equal(res[r][f"p_{step}_{i}"], res[0][f"p_{step}_{i}"])  # nodes stay in sync
+                ref_d = z[f"delta_after_{step}_{i}"][r]
+                scale = max(np.abs(ref_d).max(), lr * np.abs(z[f"grad_{step}_{i}"][r]).max())
+                np.testing.assert_allclose(res[r][f"delta_{step}_{i}"], ref_d, rtol=0, atol=2e-5 * scale)
+
+
+CHECKS = {"simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
+          "sparta_philox": check_sparta_philox, "fedavg": check_fedavg, "demo": check_demo}

@@ -1,0 +1,215 @@
+"""Multi-process strategy scenarios (one process per simulated node, gloo).
+
+Each scenario replays the harness tests/golden/gen_golden.py ran against the
+REFERENCE strategies, but through gym_amd's Strategy classes, and writes what
+each rank ends with to <out>/r<rank>.npz.  The same code runs
+  - on CPU with the oracle-backed kernel stand-ins (tests/fake_ops.py): checks
+    the host orchestration (arenas, collectives, sharding, gating, masks);
+  - on cuda:0 with the real gfx950 kernels (several ranks share the GPU over
+    gloo): strategy-level parity of the product path.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class ShapeModel(torch.nn.Module):
+    """Same construction as gen_golden.ShapeModel (so the initial values match)."""
+
+    def __init__(self, shapes, seed):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.ps = torch.nn.ParameterList(
+            [torch.nn.Parameter(torch.randn(*s, generator=g) * 0.02) for s in shapes])
+
+
+def _host(t):
+    return t.detach().float().cpu().numpy().copy()
+
+
+# ------------------------------------------------------------------ scenarios --
+def sc_simple(rank, world, dev, golden_dir):
+    from gym_amd.strategy import OptimSpec, SimpleReduceStrategy
+    z = np.load(os.path.join(golden_dir, "mean_reduce.npz"))
+    shapes = [z[f"K{world}_in_{si}"].shape[1:] for si in range(4)]
+    model = ShapeModel(shapes, seed=1).to(dev)
+    s = SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.SGD, lr=0.0))
+    s._init_node(model, rank, world)
+    s.zero_grad()
+    for si, p in enumerate(model.parameters()):
+        p.grad = torch.from_numpy(z[f"K{world}_in_{si}"][rank]).to(dev)  # not the arena view: sync_grads copies
+    s.step()
+    return {f"grad_{si}": _host(p.grad) for si, p in enumerate(model.parameters())}
+
+
+def sc_diloco(rank, world, dev, golden_dir, shard=None):
+    from gym_amd.strategy import DiLoCoStrategy, OptimSpec
+    z = np.load(os.path.join(golden_dir, "diloco.npz"))
+    ns, calls, H = int(z["nshapes"]), int(z["calls"]), int(z["H"])
+    shapes = [z[f"init_{i}"].shape for i in range(ns)]
+    model = ShapeModel(shapes, seed=1234).to(dev)
+    s = DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.SGD, lr=0.0), H=H)
+    s._init_node(model, rank, world)
+    if shard is not None:  # exercise the sharded (reduce-scatter/all-gather) path on gloo too
+        from gym_amd.engine import DiLoCoOuter
+        a = s.arena
+        s.engine = DiLoCoOuter(s.coll, 1, a.n, a.device, a.dtype, shard=shard)
+        s.engine.init_master(a.flat)
+    out = {}
+    for call in range(calls):
+        g = torch.Generator().manual_seed(1000 + 100 * rank + call)
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_((torch.randn(p.shape, generator=g) * 1e-3).to(dev))
+        s.zero_grad()
+        s.step()
+        for i, p in enumerate(model.parameters()):
+            out[f"after_{call}_{i}"] = _host(p)
+    return out
+
+
+class _ReplaySelector:
+    """Index selector that replays the masks the reference drew (rank 0's)."""
+
+    def __init__(self, z, K, shapes, p):
+        self.z, self.K, self.shapes, self.p, self.calls = z, K, shapes, p, 0
+        self.state = {}
+
+    def get_indices(self, param, iteration):
+        i = self._i
+        self._i += 1
+        n = int(np.prod(self.shapes[i]))
+        m = np.unpackbits(self.z[f"K{self.K}_mask_{iteration}_{i}"])[:n].astype(bool).reshape(self.shapes[i])
+        return torch.from_numpy(m).to(param.device)
+
+
+def sc_sparta(rank, world, dev, golden_dir, replay=True):
+    from gym_amd.strategy import OptimSpec, SPARTAStrategy
+    z = np.load(os.path.join(golden_dir, "sparta.npz"))
+    ns, calls, p = int(z["nshapes"]), int(z["calls"]), float(z["p"])
+    shapes = [z[f"K{world}_before_0_{i}"].shape[1:] for i in range(ns)]
+    torch.manual_seed(42)
+    model = ShapeModel(shapes, seed=77 + rank).to(dev)
+    s = SPARTAStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.0), p_sparta=p, mask_source="torch")
+    s._init_node(model, rank, world)
+    comm = s.communication_modules[0]
+    if replay:
+        sel = _ReplaySelector(z, world, shapes, p)
+        comm.index_selector = sel
+    out = {}
+    for call in range(calls):
+        if replay:
+            sel._i = 0
+        s.zero_grad()
+        s.step()
+        for i, prm in enumerate(model.parameters()):
+            out[f"after_{call}_{i}"] = _host(prm)
+    return out
+
+
+def sc_sparta_philox(rank, world, dev, golden_dir):
+    """Philox mode: every rank must derive the same mask; the result is
+    checked against the oracle's Philox mask + sparse average."""
+    from gym_amd.strategy import OptimSpec, SPARTAStrategy
+    shapes = [(66, 32), (128,), (96, 64), (3, 7)]
+    torch.manual_seed(42)
+    model = ShapeModel(shapes, seed=77 + rank).to(dev)
+    s = SPARTAStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.0), p_sparta=0.05)
+    s._init_node(model, rank, world)
+    out = {"before": _host(s.arena.flat)}
+    s.zero_grad()
+    s.step()
+    s.zero_grad()
+    s.step()
+    out["after"] = _host(s.arena.flat)
+    out["seed"] = np.array(s.communication_modules[0]._seed, dtype=np.int64)
+    out["n"] = np.array(s.arena.n)
+    return out
+
+
+def sc_fedavg(rank, world, dev, golden_dir, island_size=None):
+    from gym_amd.strategy import FedAvgStrategy, OptimSpec
+    shapes = [(66, 32), (128,), (3, 7)]
+    model = ShapeModel(shapes, seed=500 + rank).to(dev)
+    random.seed(1234)  # rank 0's island shuffle (the reference leaves `random` unseeded)
+    s = FedAvgStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.0), island_size=island_size, H=1)
+    s._init_node(model, rank, world)
+    out = {"before": [_host(p) for p in model.parameters()]}
+    s.zero_grad()
+    s.step()  # local_step 0: no communication
+    out["after0"] = [_host(p) for p in model.parameters()]
+    s.zero_grad()
+    s.step()  # local_step 1: average
+    out["after1"] = [_host(p) for p in model.parameters()]
+    return {f"{k}_{i}": v for k, lst in out.items() for i, v in enumerate(lst)}
+
+
+def sc_demo(rank, world, dev, golden_dir):
+    from gym_amd.strategy.communicate import all_gather
+    from gym_amd.strategy.demo_impl.demo import DeMo
+    z = np.load(os.path.join(golden_dir, "demo_steps.npz"))
+    ns, steps = int(z["nshapes"]), int(z["steps"])
+    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
+    model = ShapeModel(shapes, seed=4321).to(dev)
+    opt = DeMo(model.parameters(), compression_decay=float(z["decay"]), compression_topk=int(z["topk"]),
+               compression_chunk=int(z["chunk"]), weight_decay=float(z["wd"]), custom_all_gather=all_gather,
+               lr=float(z["lr"]))
+    out = {}
+    for step in range(steps):
+        # start every step from the reference's state (errors do not compound)
+        with torch.no_grad():
+            for i, p in enumerate(model.parameters()):
+                p.copy_(torch.from_numpy(z[f"p_before_{step}_{i}"]).to(dev))
+                opt.demo_state[p]["delta"].copy_(torch.from_numpy(z[f"delta_before_{step}_{i}"][rank]).to(dev))
+                p.grad = torch.from_numpy(z[f"grad_{step}_{i}"][rank]).to(dev)
+        opt.step()
+        for i, p in enumerate(model.parameters()):
+            out[f"p_{step}_{i}"] = _host(p)
+            out[f"delta_{step}_{i}"] = _host(opt.demo_state[p]["delta"])
+            out[f"sign_{step}_{i}"] = _host(p.grad)
+        out[f"tx_{step}"] = np.array(opt.data_transmit)
+        out[f"rx_{step}"] = np.array(opt.data_receive)
+    return out
+
+
+SCENARIOS = {"simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
+             "fedavg": sc_fedavg, "demo": sc_demo}
+
+
+def _worker(rank, world, port, name, device, fake, out_dir, golden_dir, kwargs):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    if fake:
+        import fake_ops
+        fake_ops.install()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device(device)
+        res = SCENARIOS[name](rank, world, dev, golden_dir, **kwargs)
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), **{k: np.asarray(v) for k, v in res.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def run(name, world, device, fake, out_dir, golden_dir, **kwargs):
+    import torch.multiprocessing as mp
+    port = free_port()
+    mp.spawn(_worker, args=(world, port, name, device, fake, out_dir, golden_dir, kwargs), nprocs=world, join=True)
+    res = []
+    for r in range(world):
+        with np.load(os.path.join(out_dir, f"r{r}.npz")) as f:
+            res.append({k: f[k] for k in f.files})
+    return res

@@ -1,0 +1,26 @@
+"""Multi-process (gloo, world size 2-3) runs of the Strategy classes on CPU,
+with the kernels replaced by the oracle-backed stand-ins of tests/fake_ops.py:
+checks the host orchestration of every strategy against the reference's
+golden fixtures (the GPU twin of this file, test_gpu_strategies.py, runs the
+same scenarios on the real kernels)."""
+import pytest
+
+import strategy_scenarios as S
+from conftest import GOLDEN
+from scenario_checks import CHECKS
+
+CASES = [
+    ("simple", 2, {}), ("simple", 3, {}),
+    ("diloco", 3, {}), ("diloco", 3, {"shard": True}),
+    ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": False}),
+    ("sparta_philox", 2, {}),
+    ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),
+    ("demo", 2, {}),
+]
+
+
+@pytest.mark.parametrize("name,world,kw", CASES, ids=[f"{c[0]}-w{c[1]}-{c[2]}" for c in CASES])
+def test_strategy_orchestration_gloo(tmp_path, name, world, kw):
+    res = S.run(name, world, "cpu", True, str(tmp_path), GOLDEN, **kw)
+    check_kw = {"island_size": kw["island_size"]} if "island_size" in kw else {}
+    CHECKS[name](res, world, GOLDEN, **check_kw)
