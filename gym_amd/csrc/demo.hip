@@ -77,8 +77,9 @@ __device__ __forceinline__ int find_tensor(const ga_demo_tensor* T, int ntens, i
     return *slot;
 }
 
-// Exclusive scan of one int per lane over the 256-lane workgroup.
-__device__ __forceinline__ int scan256(int v, int* wave_tot) {
+// Exclusive scan of one int per lane over the 256-lane workgroup (optionally
+// the total).
+__device__ __forceinline__ int scan256(int v, int* wave_tot, int* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int x = v;
 #pragma unroll
@@ -88,95 +89,147 @@ __device__ __forceinline__ int scan256(int v, int* wave_tot) {
     }
     if (lane == 63) wave_tot[wid] = x;
     __syncthreads();
-    int pre = 0;
+    int pre = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) pre += (w < wid) ? wave_tot[w] : 0;
+    for (int w = 0; w < 4; ++w) {
+        pre += (w < wid) ? wave_tot[w] : 0;
+        tot += wave_tot[w];
+    }
     __syncthreads();
+    if (total) *total = tot;
     return pre + x - v;
 }
 
+// ---- chunk I/O: lane t owns rows (t>>4) + 16i (i < 4), columns 4(t&15) .. +3 ----
+struct ChunkIO {
+    int64_t base;  // element offset of the chunk's (0, 0)
+    int cols, n1, n2;
+    bool vec;      // 4-element vector accesses are legal for this tensor
+    __device__ __forceinline__ int row(int i) const { return (threadIdx.x >> 4) + 16 * i; }
+    __device__ __forceinline__ int col0() const { return 4 * (threadIdx.x & 15); }
+    __device__ __forceinline__ bool live(int i) const { return row(i) < n1 && col0() < n2; }
+    __device__ __forceinline__ int64_t addr(int i) const { return base + (int64_t)row(i) * cols + col0(); }
+};
+
 template <typename T>
-__global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
-    const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ F,
-    const float* __restrict__ B, T* param, const T* __restrict__ grad, T* delta, int64_t ld, float lr,
-    float decay, float wd_factor, int32_t* payload, int64_t pstride, int64_t M) {
-    __shared__ float X[kTile];
-    __shared__ float Y[kTile];
-    __shared__ int hist[256];
-    __shared__ int misc[8];
-
-    const int chunk = blockIdx.x;
-    const int tix = find_tensor(tens, ntens, chunk, &misc[0]);
-    const ga_demo_tensor td = tens[tix];
-    const int c = chunk - td.chunk_start;
-    const int cy = c / td.gx, cx = c - cy * td.gx;
-    const int64_t rep = blockIdx.y;
-    param += rep * ld;
-    grad += rep * ld;
-    delta += rep * ld;
-    payload += rep * pstride;
-    const int64_t base = td.offset + (int64_t)cy * td.n1 * td.cols + (int64_t)cx * td.n2;
-    const int n1 = td.n1, n2 = td.n2;
-
-    // 1. error feedback: delta = decay*delta + lr*grad (and the decoupled weight decay)
-    for (int e = threadIdx.x; e < 4096; e += kDmBlock) {
-        const int h = e >> 6, w = e & 63;
-        float v = 0.f;
-        if (h < n1 && w < n2) {
-            const int64_t a = base + (int64_t)h * td.cols + w;
-            if (wd_factor != 1.f) Elem<T>::store(param + a, Elem<T>::load(param + a) * wd_factor);
-            float d = Elem<T>::load(delta + a);
-            if (decay != 1.f) d = d * decay;
-            v = fmaf(lr, Elem<T>::load(grad + a), d);
-        }
-        X[h * kLd + w] = v;
-    }
-    __syncthreads();
-
-    // 2. Y = F1^T . X . F2
-    f32x16 acc = mm64<true, false>(X, F + (int64_t)td.basis2 * 4096);
-    store_acc(Y, acc);
-    __syncthreads();
-    acc = mm64<false, true>(F + (int64_t)td.basis1 * 4096, Y);
-    __syncthreads();
-    store_acc(Y, acc);
-    __syncthreads();
-
-    // 3. top-k of |Y| over the valid n1 x n2 region; lane t owns coefficients
-    //    16t .. 16t+15 of the padded row-major 64x64 grid.
-    const int row = threadIdx.x >> 2, col0 = 16 * (threadIdx.x & 3);
-    uint32_t key[16];
+__device__ __forceinline__ void load4(const T* p, const ChunkIO& io, int i, float (&v)[4]) {
+    if (io.vec) {
+        Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(p + io.addr(i)), v);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const bool valid = row < n1 && (col0 + j) < n2;
-        key[j] = valid ? (__float_as_uint(Y[row * kLd + col0 + j]) & 0x7fffffffu) + 1u : 0u;
+        for (int c = 0; c < 4; ++c) v[c] = (io.col0() + c < io.n2) ? Elem<T>::load(p + io.addr(i) + c) : 0.f;
     }
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const ChunkIO& io, int i, const float (&v)[4]) {
+    if (io.vec) {
+        *reinterpret_cast<typename Vec4<T>::type*>(p + io.addr(i)) = Vec4<T>::pack(v);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (io.col0() + c < io.n2) Elem<T>::store(p + io.addr(i) + c, v[c]);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ ChunkIO chunk_io(const ga_demo_tensor& td, int c, int64_t ld, bool ptr_vec) {
+    ChunkIO io;
+    const int cy = c / td.gx, cx = c - cy * td.gx;
+    io.base = td.offset + (int64_t)cy * td.n1 * td.cols + (int64_t)cx * td.n2;
+    io.cols = td.cols;
+    io.n1 = td.n1;
+    io.n2 = td.n2;
+    io.vec = ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0) && (td.n2 % 4 == 0) && (ld % 4 == 0);
+    return io;
+}
+
+constexpr int kCandMax = 1024;   // candidate list of the threshold top-k
+constexpr int kEntMax = 2048;    // entries per chunk supported by the residual (topk <= 2048)
+constexpr int kStage = 32;       // entries staged per residual pass
+
+// Selection bits (T-map: lane t owns coefficients 16t .. 16t+15 of the padded
+// row-major grid) of the k largest keys; ties at the k-th key -> lowest index.
+// Fast path: T0 = the k-th largest of the 256 per-lane maxima is a lower bound
+// on the k-th largest key (>= k lanes hold a key >= T0), so the answer lies
+// among the keys >= T0; they are ranked exactly in LDS.  Falls back to a
+// 4-round 8-bit radix select when k > 256 or there are too many candidates
+// (e.g. an all-zero chunk, where every key ties).
+__device__ uint32_t select_topk(const uint32_t (&key)[16], int k, uint32_t* tmax, uint32_t* cand_key,
+                                uint8_t* cand_sel, int* hist, int* misc) {
+    const int t = threadIdx.x;
+    uint32_t mymax = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mymax = key[j] > mymax ? key[j] : mymax;
+    bool fast = k <= kDmBlock;
+    uint32_t sel = 0;
+    if (fast) {
+        tmax[t] = mymax;
+        __syncthreads();
+        int r = 0;
+        for (int j = 0; j < kDmBlock; ++j) {
+            const uint32_t o = tmax[j];
+            r += (o > mymax) | ((o == mymax) & (j < t));
+        }
+        if (r == k - 1) misc[1] = (int)mymax;
+        __syncthreads();
+        uint32_t T0 = (uint32_t)misc[1];
+        if (T0 == 0u) T0 = 1u;  // key 0 marks padding; small chunks rank all their keys
+        int cc = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) cc += key[j] >= T0;
+        int C;
+        const int cbase = scan256(cc, misc + 4, &C);
+        fast = C <= kCandMax;
+        if (fast) {
+            int w = cbase;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (key[j] >= T0) cand_key[w++] = key[j];
+            __syncthreads();
+            for (int i = t; i < C; i += kDmBlock) {
+                const uint32_t ki = cand_key[i];
+                int rank = 0;
+                for (int j = 0; j < C; ++j) {
+                    const uint32_t kj = cand_key[j];
+                    rank += (kj > ki) | ((kj == ki) & (j < i));
+                }
+                cand_sel[i] = rank < k;
+            }
+            __syncthreads();
+            w = cbase;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (key[j] >= T0) sel |= (uint32_t)cand_sel[w++] << j;
+            return sel;
+        }
+    }
+    // radix select of the k-th largest key
     uint32_t prefix = 0, pmask = 0;
-    int kk = td.k;
+    int kk = k;
     for (int shift = 24; shift >= 0; shift -= 8) {
-        hist[threadIdx.x] = 0;
+        hist[t] = 0;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 16; ++j)
             if ((key[j] & pmask) == prefix) atomicAdd(&hist[(key[j] >> shift) & 255u], 1);
         __syncthreads();
-        if (threadIdx.x < 64) {
-            const int lane = threadIdx.x;
+        if (t < 64) {
             int hb[4];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) hb[b] = hist[4 * lane + b];
+            for (int b = 0; b < 4; ++b) hb[b] = hist[4 * t + b];
             const int lsum = hb[0] + hb[1] + hb[2] + hb[3];
             int x = lsum;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const int y = __shfl_down(x, d, 64);
-                if (lane + d < 64) x += y;
+                if (t + d < 64) x += y;
             }
-            int cum = x - lsum;  // count in bins above this lane's bins
+            int cum = x - lsum;
 #pragma unroll
             for (int b = 3; b >= 0; --b) {
                 if (cum < kk && cum + hb[b] >= kk) {
-                    misc[1] = 4 * lane + b;
+                    misc[1] = 4 * t + b;
                     misc[2] = kk - cum;
                 }
                 cum += hb[b];
@@ -188,13 +241,10 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
         kk = misc[2];
         __syncthreads();
     }
-    // prefix == key of the k-th largest magnitude; take every larger key and
-    // the first kk keys equal to it in coefficient order.
     int eq = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) eq += key[j] == prefix;
-    int eq_run = scan256(eq, &misc[4]);
-    uint32_t sel = 0;
+    int eq_run = scan256(eq, misc + 4, nullptr);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         if (key[j] > prefix) sel |= 1u << j;
@@ -203,35 +253,138 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
             ++eq_run;
         }
     }
-    int slot = scan256(__popc(sel), &misc[4]);
-    int32_t* out_idx = payload + td.payload_off + (int64_t)c * td.k;
-    float* out_val = reinterpret_cast<float*>(payload + M) + td.payload_off + (int64_t)c * td.k;
+    return sel;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
+    const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ F,
+    const float* __restrict__ B, T* param, const T* __restrict__ grad, T* delta, int64_t ld, float lr,
+    float decay, float wd_factor, int32_t* payload, int64_t pstride, int64_t M, int ptr_vec) {
+    __shared__ float X[kTile];   // delta chunk (MFMA A operand); then the entry list
+    __shared__ float Y[kTile];   // T = X.F2, Y = F1^T.T; then the residual staging
+    __shared__ uint32_t tmax[kDmBlock];
+    __shared__ uint32_t cand_key[kCandMax];
+    __shared__ uint8_t cand_sel[kCandMax];
+    __shared__ int hist[256];
+    __shared__ int misc[8];
+
+    const int chunk = blockIdx.x;
+    const int tix = find_tensor(tens, ntens, chunk, &misc[0]);
+    const ga_demo_tensor td = tens[tix];
+    const int c = chunk - td.chunk_start;
+    const int64_t rep = blockIdx.y;
+    param += rep * ld;
+    grad += rep * ld;
+    delta += rep * ld;
+    payload += rep * pstride;
+    const ChunkIO io = chunk_io<T>(td, c, ld, ptr_vec != 0);
+    const int n1 = td.n1, n2 = td.n2, k = td.k;
+
+    // 1. error feedback in registers: x = decay*delta + lr*grad (+ decoupled weight decay on p)
+    float x[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (io.live(i)) {
+            float d[4], g[4];
+            load4(delta, io, i, d);
+            load4(grad, io, i, g);
+            if (wd_factor != 1.f) {
+                float p[4];
+                load4(param, io, i, p);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) p[e] *= wd_factor;
+                store4(param, io, i, p);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[i][e] = fmaf(lr, g[e], decay != 1.f ? d[e] * decay : d[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[i][e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) X[io.row(i) * kLd + io.col0() + e] = (io.col0() + e < n2) ? x[i][e] : 0.f;
+    }
+    __syncthreads();
+
+    // 2. Y = F1^T . X . F2 on the matrix cores
+    f32x16 acc = mm64<true, false>(X, F + (int64_t)td.basis2 * 4096);
+    store_acc(Y, acc);
+    __syncthreads();
+    acc = mm64<false, true>(F + (int64_t)td.basis1 * 4096, Y);
+    __syncthreads();
+    store_acc(Y, acc);
+    __syncthreads();
+
+    // 3. top-k of |Y| over the valid n1 x n2 coefficients
+    const int row = threadIdx.x >> 2, col0 = 16 * (threadIdx.x & 3);
+    uint32_t key[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        float& y = Y[row * kLd + col0 + j];
+        const bool valid = row < n1 && (col0 + j) < n2;
+        key[j] = valid ? (__float_as_uint(Y[row * kLd + col0 + j]) & 0x7fffffffu) + 1u : 0u;
+    }
+    const uint32_t sel = select_topk(key, k, tmax, cand_key, cand_sel, hist, misc);
+
+    // 4. emit the entries in ascending coefficient order; keep (b, d, v) in LDS
+    int* ent_bd = reinterpret_cast<int*>(X);
+    float* ent_v = X + kEntMax;
+    int slot = scan256(__popc(sel), misc + 4, nullptr);
+    int32_t* out_idx = payload + td.payload_off + (int64_t)c * k;
+    float* out_val = reinterpret_cast<float*>(payload + M) + td.payload_off + (int64_t)c * k;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
         if (sel & (1u << j)) {
+            const float y = Y[row * kLd + col0 + j];
             out_idx[slot] = row * n2 + col0 + j;
             out_val[slot] = y;
+            ent_bd[slot] = (row << 8) | (col0 + j);
+            ent_v[slot] = y;
             ++slot;
-        } else {
-            y = 0.f;  // Y becomes the sparse S of the kept coefficients
         }
     }
     __syncthreads();
 
-    // 4. delta -= B1^T . S . B2  (the estimate of what was transmitted)
-    acc = mm64<true, false>(Y, B + (int64_t)td.basis2 * 4096);
-    __syncthreads();
-    store_acc(Y, acc);
-    __syncthreads();
-    acc = mm64<false, true>(B + (int64_t)td.basis1 * 4096, Y);
-    const int cc = acc_col();
+    // 5. residual: delta = x - sum_e v_e * outer(B1[b_e, :], B2[d_e, :])  (the sparse
+    //    form of B1^T . S . B2: k rank-1 terms instead of two dense products)
+    float r[4][4];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rr = acc_row(r);
-        if (rr < n1 && cc < n2) {
-            const int64_t a = base + (int64_t)rr * td.cols + cc;
-            Elem<T>::store(delta + a, X[rr * kLd + cc] - acc[r]);
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[i][e] = 0.f;
+    const float* B1 = B + (int64_t)td.basis1 * 4096;
+    const float* B2 = B + (int64_t)td.basis2 * 4096;
+    float* U = Y;                 // [kStage][64]: v_e * B1[b_e, h]
+    float* W = Y + kStage * 64;   // [kStage][64]: B2[d_e, w]
+    for (int e0 = 0; e0 < k; e0 += kStage) {
+        const int ne = (k - e0) < kStage ? (k - e0) : kStage;
+        for (int f = threadIdx.x; f < ne * 128; f += kDmBlock) {
+            const int e = f >> 7, cidx = f & 127;
+            const int bd = ent_bd[e0 + e];
+            if (cidx < 64) U[e * 64 + cidx] = ent_v[e0 + e] * B1[(bd >> 8) * 64 + cidx];
+            else W[e * 64 + cidx - 64] = B2[(bd & 255) * 64 + cidx - 64];
+        }
+        __syncthreads();
+        for (int e = 0; e < ne; ++e) {
+            const float4 wv = *reinterpret_cast<const float4*>(W + e * 64 + io.col0());
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float u = U[e * 64 + io.row(i)];
+                r[i][0] = fmaf(u, wv.x, r[i][0]);
+                r[i][1] = fmaf(u, wv.y, r[i][1]);
+                r[i][2] = fmaf(u, wv.z, r[i][2]);
+                r[i][3] = fmaf(u, wv.w, r[i][3]);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (io.live(i)) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = x[i][e] - r[i][e];
+            store4(delta, io, i, o);
         }
     }
 }
@@ -240,7 +393,7 @@ template <typename T>
 __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ B,
     const int32_t* __restrict__ payload, int64_t pstride, int64_t M, int64_t nsrc, T* param, T* grad,
-    int64_t K, int64_t ld, float lr) {
+    int64_t K, int64_t ld, float lr, int ptr_vec) {
     __shared__ float S[kTile];
     __shared__ int cnt[4096];
     __shared__ int misc[4];
@@ -249,9 +402,8 @@ __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
     const int tix = find_tensor(tens, ntens, chunk, &misc[0]);
     const ga_demo_tensor td = tens[tix];
     const int c = chunk - td.chunk_start;
-    const int cy = c / td.gx, cx = c - cy * td.gx;
-    const int n1 = td.n1, n2 = td.n2, nk = td.k, nvalid = n1 * n2;
-    const int64_t base = td.offset + (int64_t)cy * n1 * td.cols + (int64_t)cx * n2;
+    const int n2 = td.n2, nk = td.k, nvalid = td.n1 * td.n2;
+    const ChunkIO io = chunk_io<T>(td, c, ld, ptr_vec != 0);
 
     for (int e = threadIdx.x; e < kTile; e += kDmBlock) S[e] = 0.f;
     for (int e = threadIdx.x; e < 4096; e += kDmBlock) cnt[e] = 0;
@@ -280,25 +432,33 @@ __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
     }
     __syncthreads();
 
-    // g = B1^T . S . B2;  grad = sign(g);  p -= lr * grad   (demo.py:192-209)
+    // g = B1^T . S . B2 on the matrix cores, staged back through LDS for row-major I/O
     f32x16 acc = mm64<true, false>(S, B + (int64_t)td.basis2 * 4096);
     __syncthreads();
     store_acc(S, acc);
     __syncthreads();
     acc = mm64<false, true>(B + (int64_t)td.basis1 * 4096, S);
-    const int cc = acc_col();
+    __syncthreads();
+    store_acc(S, acc);
+    __syncthreads();
+
+    // grad = sign(g) (torch.sign: NaN -> 0);  p -= lr * grad   (demo.py:200-209)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rr = acc_row(r);
-        if (rr < n1 && cc < n2) {
-            const float g = acc[r];
-            const float sg = (float)((g > 0.f) - (g < 0.f));  // torch.sign: NaN -> 0
-            const int64_t a = base + (int64_t)rr * td.cols + cc;
-            for (int64_t k = 0; k < K; ++k) {
-                T* p = param + k * ld + a;
-                Elem<T>::store(p, fmaf(-lr, sg, Elem<T>::load(p)));
-                if (grad) Elem<T>::store(grad + k * ld + a, sg);
-            }
+    for (int i = 0; i < 4; ++i) {
+        if (!io.live(i)) continue;
+        float sg[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float g = S[io.row(i) * kLd + io.col0() + e];
+            sg[e] = (float)((g > 0.f) - (g < 0.f));
+        }
+        for (int64_t k = 0; k < K; ++k) {
+            float p[4];
+            load4(param + k * ld, io, i, p);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) p[e] = fmaf(-lr, sg[e], p[e]);
+            store4(param + k * ld, io, i, p);
+            if (grad) store4(grad + k * ld, io, i, sg);
         }
     }
 }
@@ -324,17 +484,19 @@ extern "C" GA_API int ga_demo_encode(int dtype, const ga_demo_tensor* tensors, i
     GA_REQUIRE(tensors && F && B && param && grad && delta && payload, "ga_demo_encode: null buffer");
     GA_REQUIRE(K >= 1 && K <= 65535, "ga_demo_encode: K=%lld out of range", (long long)K);
     GA_REQUIRE(K == 1 || (ld > 0 && payload_stride >= 2 * M), "ga_demo_encode: bad replica strides");
+    const int vb = dtype == GA_F32 ? 16 : 8;
+    const int ptr_vec = ((uintptr_t)param % vb == 0) && ((uintptr_t)grad % vb == 0) && ((uintptr_t)delta % vb == 0);
     dim3 grid((unsigned)nchunks, (unsigned)K);
     switch (dtype) {
         case GA_F32:
             hipLaunchKernelGGL((demo_encode_kernel<float>), grid, dim3(kDmBlock), 0, stream, tensors, ntensors, F, B,
                                (float*)param, (const float*)grad, (float*)delta, ld, lr, decay, wd_factor, payload,
-                               payload_stride, M);
+                               payload_stride, M, ptr_vec);
             break;
         case GA_BF16:
             hipLaunchKernelGGL((demo_encode_kernel<__hip_bfloat16>), grid, dim3(kDmBlock), 0, stream, tensors,
                                ntensors, F, B, (__hip_bfloat16*)param, (const __hip_bfloat16*)grad,
-                               (__hip_bfloat16*)delta, ld, lr, decay, wd_factor, payload, payload_stride, M);
+                               (__hip_bfloat16*)delta, ld, lr, decay, wd_factor, payload, payload_stride, M, ptr_vec);
             break;
         default: set_error("ga_demo_encode: unknown dtype %d", dtype); return GA_EINVAL;
     }
@@ -351,16 +513,18 @@ extern "C" GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, i
     GA_REQUIRE(S >= 1 && K >= 1, "ga_demo_decode: bad S=%lld K=%lld", (long long)S, (long long)K);
     GA_REQUIRE(S == 1 || payload_stride >= 2 * M, "ga_demo_decode: payload_stride < 2*M");
     GA_REQUIRE(K == 1 || ld > 0, "ga_demo_decode: bad ld");
+    const int vb = dtype == GA_F32 ? 16 : 8;
+    const int ptr_vec = ((uintptr_t)param % vb == 0) && (grad == nullptr || (uintptr_t)grad % vb == 0);
     switch (dtype) {
         case GA_F32:
             hipLaunchKernelGGL((demo_decode_kernel<float>), dim3((unsigned)nchunks), dim3(kDmBlock), 0, stream,
                                tensors, ntensors, B, payload, payload_stride, M, S, (float*)param, (float*)grad, K,
-                               ld, lr);
+                               ld, lr, ptr_vec);
             break;
         case GA_BF16:
             hipLaunchKernelGGL((demo_decode_kernel<__hip_bfloat16>), dim3((unsigned)nchunks), dim3(kDmBlock), 0,
                                stream, tensors, ntensors, B, payload, payload_stride, M, S, (__hip_bfloat16*)param,
-                               (__hip_bfloat16*)grad, K, ld, lr);
+                               (__hip_bfloat16*)grad, K, ld, lr, ptr_vec);
             break;
         default: set_error("ga_demo_decode: unknown dtype %d", dtype); return GA_EINVAL;
     }

@@ -102,38 +102,66 @@ __global__ __launch_bounds__(kSpBlock) void sparta_count_kernel(Pred P, int64_t 
 }
 
 // One workgroup: exclusive scan of the tile counts -> tile offsets, total and
-// the overflow flag.
+// the overflow flag.  The counts are staged through LDS in coalesced passes of
+// kScanChunk tiles (all loads in flight at once), then each lane scans a
+// contiguous run of its pass from LDS.
+constexpr int kScanChunk = 16384;
+
 __global__ __launch_bounds__(kScanBlock) void sparta_scan_kernel(const int32_t* tile_counts, int64_t ntiles,
                                                                  int32_t* tile_offsets, int64_t cap,
                                                                  int64_t* count) {
+    __shared__ int32_t buf[kScanChunk];
     __shared__ int64_t wave_tot[kScanBlock / 64];
-    const int64_t per = (ntiles + kScanBlock - 1) / kScanBlock;
-    const int64_t b0 = (int64_t)threadIdx.x * per;
-    int64_t s = 0;
-    for (int64_t i = 0; i < per && b0 + i < ntiles; ++i) s += tile_counts[b0 + i];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int64_t x = s;
-    for (int d = 1; d < 64; d <<= 1) {
-        const int64_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) wave_tot[wid] = x;
-    __syncthreads();
-    int64_t pre = 0, tot = 0;
-    for (int w = 0; w < kScanBlock / 64; ++w) {
-        pre += (w < wid) ? wave_tot[w] : 0;
-        tot += wave_tot[w];
-    }
-    int64_t run = pre + x - s;
-    for (int64_t i = 0; i < per && b0 + i < ntiles; ++i) {
-        tile_offsets[b0 + i] = (int32_t)run;
-        run += tile_counts[b0 + i];
+    constexpr int per = kScanChunk / kScanBlock;  // 16 tiles per lane per pass
+    int64_t carry = 0;
+    for (int64_t base = 0; base < ntiles; base += kScanChunk) {
+        const int64_t m = (ntiles - base) < kScanChunk ? (ntiles - base) : kScanChunk;
+        for (int i = threadIdx.x; i < kScanChunk; i += kScanBlock) buf[i] = i < m ? tile_counts[base + i] : 0;
+        __syncthreads();
+        int32_t v[per];
+        int64_t s = 0;
+#pragma unroll
+        for (int i = 0; i < per; ++i) {
+            v[i] = buf[threadIdx.x * per + i];
+            s += v[i];
+        }
+        int64_t x = s;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wave_tot[wid] = x;
+        __syncthreads();
+        int64_t pre = carry, tot = 0;
+        for (int w = 0; w < kScanBlock / 64; ++w) {
+            pre += (w < wid) ? wave_tot[w] : 0;
+            tot += wave_tot[w];
+        }
+        int64_t run = pre + x - s;
+#pragma unroll
+        for (int i = 0; i < per; ++i) {
+            buf[threadIdx.x * per + i] = (int32_t)run;
+            run += v[i];
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < m; i += kScanBlock) tile_offsets[base + i] = buf[i];
+        carry += tot;
+        __syncthreads();
     }
     if (threadIdx.x == 0) {
-        count[0] = tot;
-        count[1] = tot > cap ? 1 : 0;
+        count[0] = carry;
+        count[1] = carry > cap ? 1 : 0;
     }
 }
+
+// Select + gather.  The workgroup recomputes its tile's predicate, scans it
+// to output positions, lists its selected elements in LDS, then all 256 lanes
+// load the (element, replica) pairs densely (one load per lane, no idle lanes
+// on sparse tiles) into LDS, and one lane per element sums its K values in
+// ascending replica order.
+constexpr int kGatherSlots = 2048;  // floats of LDS for the (element, replica) values
 
 template <typename T>
 __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t n, const int32_t* tile_offsets,
@@ -141,23 +169,55 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
                                                                  int64_t cap, int32_t* __restrict__ idx,
                                                                  T* __restrict__ vals) {
     __shared__ int wave_tot[4];
-    const int64_t e0 = (int64_t)blockIdx.x * kSpTile + (int64_t)threadIdx.x * kSpPerThread;
+    __shared__ int32_t sel_list[kSpTile];
+    __shared__ float gv[kGatherSlots];
+    const int64_t tile0 = (int64_t)blockIdx.x * kSpTile;
+    const int64_t e0 = tile0 + (int64_t)threadIdx.x * kSpPerThread;
     uint32_t bits = e0 < n ? pred_bits16(P, e0, n) : 0u;
-    int pos = block_excl_scan_256(__popc(bits), wave_tot, nullptr) + tile_offsets[blockIdx.x];
+    int total;
+    int local = block_excl_scan_256(__popc(bits), wave_tot, &total);
+    const int64_t out0 = tile_offsets[blockIdx.x];
     while (bits) {
         const int j = __ffs(bits) - 1;
         bits &= bits - 1;
-        if (pos < cap) {
-            const int64_t i = e0 + j;
+        const int32_t i = (int32_t)(threadIdx.x * kSpPerThread + j);
+        sel_list[local] = i;
+        const int64_t pos = out0 + local;
+        if (pos < cap) idx[pos] = (int32_t)(tile0 + i);
+        ++local;
+    }
+    __syncthreads();
+    // entries per pass: as many as fit K values each in the LDS slots
+    const int per_pass = K >= kGatherSlots ? 1 : (kGatherSlots / K < kSpBlock ? kGatherSlots / (int)K : kSpBlock);
+    for (int c0 = 0; c0 < total; c0 += per_pass) {
+        const int ce = (total - c0) < per_pass ? (total - c0) : per_pass;
+        if (K <= kGatherSlots) {
+            const int Ki = (int)K;
+            for (int f = threadIdx.x; f < ce * Ki; f += kSpBlock) {
+                const int e = f / Ki, k = f - e * Ki;
+                gv[f] = Elem<T>::load(src + (int64_t)k * ld + tile0 + sel_list[c0 + e]);
+            }
+            __syncthreads();
+            if (threadIdx.x < ce) {
+                float acc = 0.f;
+                for (int64_t k = 0; k < K; ++k) acc += gv[threadIdx.x * K + k];
+                const int64_t pos = out0 + c0 + threadIdx.x;
+                if (pos < cap) Elem<T>::store(vals + pos, acc);
+            }
+            __syncthreads();
+        } else {  // very many replicas: one element at a time, lanes over replicas
+            const int64_t i = tile0 + sel_list[c0];
             float acc = 0.f;
-            for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + k * ld + i);
-            idx[pos] = (int32_t)i;
-            Elem<T>::store(vals + pos, acc);
+            if (threadIdx.x == 0)
+                for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + k * ld + i);
+            const int64_t pos = out0 + c0;
+            if (threadIdx.x == 0 && pos < cap) Elem<T>::store(vals + pos, acc);
         }
-        ++pos;
     }
 }
 
+// Scatter: one lane per (element, replica) pair, so every lane stores;
+// replicas on the grid's y dimension (no per-lane division).
 template <typename T>
 __global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __restrict__ vals,
                                                                   const int32_t* __restrict__ idx,
@@ -165,10 +225,10 @@ __global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __res
                                                                   float divisor, T* dst, int64_t K, int64_t ld) {
     const int64_t m = count[0] < cap ? count[0] : cap;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
-        const float v = Elem<T>::load(vals + j) / divisor;
-        const int64_t i = idx[j];
-        for (int64_t k = 0; k < K; ++k) Elem<T>::store(dst + k * ld + i, v);
+    for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
+        T* d = dst + k * ld;
+        for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride)
+            Elem<T>::store(d + idx[j], Elem<T>::load(vals + j) / divisor);
     }
 }
 
@@ -241,14 +301,15 @@ extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32
     if (cap == 0) return GA_OK;
     GA_REQUIRE(vals && idx && count && dst, "ga_sparta_scatter: null buffer");
     GA_REQUIRE(divisor != 0.0f, "ga_sparta_scatter: divisor is 0");
-    const int grid = stream_grid(cap, kSpBlock);
+    const int gx = stream_grid(cap, kSpBlock);
+    const dim3 grid(gx > 64 ? 64 : gx, (unsigned)(K < 65535 ? K : 65535));
     switch (dtype) {
         case GA_F32:
-            hipLaunchKernelGGL((sparta_scatter_kernel<float>), dim3(grid), dim3(kSpBlock), 0, stream,
+            hipLaunchKernelGGL((sparta_scatter_kernel<float>), grid, dim3(kSpBlock), 0, stream,
                                (const float*)vals, idx, count, cap, divisor, (float*)dst, K, ld);
             break;
         case GA_BF16:
-            hipLaunchKernelGGL((sparta_scatter_kernel<__hip_bfloat16>), dim3(grid), dim3(kSpBlock), 0, stream,
+            hipLaunchKernelGGL((sparta_scatter_kernel<__hip_bfloat16>), grid, dim3(kSpBlock), 0, stream,
                                (const __hip_bfloat16*)vals, idx, count, cap, divisor, (__hip_bfloat16*)dst, K, ld);
             break;
         default: set_error("ga_sparta_scatter: unknown dtype %d", dtype); return GA_EINVAL;

@@ -1,0 +1,168 @@
+// Micro-benchmark of streaming-kernel variants for the fused DiLoCo outer step
+// ([K, n] replicas + master + momentum, fp32).  Standalone: hipcc -O3
+// --offload-arch=gfx950 tools/ubench_diloco.hip -o build/ubench_diloco
+// Prints GB/s of algorithmic bytes for each variant, and a float4 copy for
+// calibration.  Not part of the library.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+struct OP { float divisor, lr, mu; };
+
+__device__ __forceinline__ float upd(float s, float& m, float& b, const OP& op) {
+    float avg = s / op.divisor;
+    float g = m - avg;
+    b = fmaf(1.f, g, b * op.mu);
+    g = fmaf(op.mu, b, g);
+    m = fmaf(-op.lr, g, m);
+    return m;
+}
+
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float4* p) {
+    if constexpr (NT) {
+        float4 r;
+        r.x = __builtin_nontemporal_load(&p->x);
+        r.y = __builtin_nontemporal_load(&p->y);
+        r.z = __builtin_nontemporal_load(&p->z);
+        r.w = __builtin_nontemporal_load(&p->w);
+        return r;
+    } else {
+        return *p;
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float4* p, float4 v) {
+    if constexpr (NT) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+        __builtin_nontemporal_store(v.z, &p->z);
+        __builtin_nontemporal_store(v.w, &p->w);
+    } else {
+        *p = v;
+    }
+}
+
+// runtime K (the library's current form)
+__global__ __launch_bounds__(256) void v_runtime(const float* src, long K, long ld, long n, float* master, float* mom,
+                                                 OP op, float* dst) {
+    long stride = (long)gridDim.x * blockDim.x;
+    long nv = n >> 2;
+    for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        float a[4] = {0, 0, 0, 0};
+#pragma unroll 4
+        for (long k = 0; k < K; ++k) {
+            float4 x = reinterpret_cast<const float4*>(src + k * ld)[v];
+            a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w;
+        }
+        float4 m = reinterpret_cast<float4*>(master)[v], b = reinterpret_cast<float4*>(mom)[v];
+        float4 o;
+        o.x = upd(a[0], m.x, b.x, op); o.y = upd(a[1], m.y, b.y, op);
+        o.z = upd(a[2], m.z, b.z, op); o.w = upd(a[3], m.w, b.w, op);
+        reinterpret_cast<float4*>(master)[v] = m;
+        reinterpret_cast<float4*>(mom)[v] = b;
+        for (long k = 0; k < K; ++k) reinterpret_cast<float4*>(dst + k * ld)[v] = o;
+    }
+}
+
+// compile-time K, U vectors per lane per iteration, optional nontemporal loads/stores
+template <int K, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void v_static(const float* src, long ld, long n, float* master, float* mom, OP op,
+                                                float* dst) {
+    long stride = (long)gridDim.x * blockDim.x * U;
+    long nv = n >> 2;
+    for (long v0 = ((long)blockIdx.x * blockDim.x) * U + threadIdx.x; v0 < nv; v0 += stride) {
+        float4 x[U][K];
+        float4 m[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            long v = v0 + (long)u * blockDim.x;
+            if (v < nv) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) x[u][k] = ld4<NTL>(reinterpret_cast<const float4*>(src + k * ld) + v);
+                m[u] = ld4<NTL>(reinterpret_cast<const float4*>(master) + v);
+                b[u] = ld4<NTL>(reinterpret_cast<const float4*>(mom) + v);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            long v = v0 + (long)u * blockDim.x;
+            if (v < nv) {
+                float a[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < K; ++k) { a[0] += x[u][k].x; a[1] += x[u][k].y; a[2] += x[u][k].z; a[3] += x[u][k].w; }
+                float4 o;
+                o.x = upd(a[0], m[u].x, b[u].x, op); o.y = upd(a[1], m[u].y, b[u].y, op);
+                o.z = upd(a[2], m[u].z, b[u].z, op); o.w = upd(a[3], m[u].w, b[u].w, op);
+                st4<NTS>(reinterpret_cast<float4*>(master) + v, m[u]);
+                st4<NTS>(reinterpret_cast<float4*>(mom) + v, b[u]);
+#pragma unroll
+                for (int k = 0; k < K; ++k) st4<NTS>(reinterpret_cast<float4*>(dst + k * ld) + v, o);
+            }
+        }
+    }
+}
+
+__global__ void copy4(const float4* a, float4* b, long nv) {
+    long stride = (long)gridDim.x * blockDim.x;
+    for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) b[v] = a[v];
+}
+
+template <typename F>
+float time_ms(F f, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) f();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / reps;
+}
+
+int main() {
+    const int K = 8;
+    const long n = 124475904;  // GPT-2 124M arena
+    const long ld = n;
+    float *src, *master, *mom;
+    CK(hipMalloc(&src, sizeof(float) * K * ld));
+    CK(hipMalloc(&master, sizeof(float) * n));
+    CK(hipMalloc(&mom, sizeof(float) * n));
+    CK(hipMemset(src, 0, sizeof(float) * K * ld));
+    CK(hipMemset(master, 0, sizeof(float) * n));
+    CK(hipMemset(mom, 0, sizeof(float) * n));
+    OP op{8.f, 0.7f, 0.9f};
+    const double bytes = (2.0 * K + 4.0) * 4.0 * n;
+    const int reps = 20;
+    {
+        float* cdst;
+        CK(hipMalloc(&cdst, sizeof(float) * 2 * n));
+        for (int g : {1024, 2048, 4096, 8192}) {
+            float ms = time_ms([&] { copy4<<<g, 256>>>((const float4*)src, (float4*)cdst, 2 * n / 4); }, reps);
+            printf("copy float4 2x%.0fMB grid %5d: %.3f ms  %.0f GB/s\n", 4.0 * n / 1e6, g, ms, 2 * 8.0 * n / ms / 1e6);
+        }
+        CK(hipFree(cdst));
+    }
+    for (int g : {2048, 4096, 8192}) {
+        float ms = time_ms([&] { v_runtime<<<g, 256>>>(src, K, ld, n, master, mom, op, src); }, reps);
+        printf("runtime-K       grid %5d: %.3f ms  %.0f GB/s\n", g, ms, bytes / ms / 1e6);
+    }
+#define RUN(U, NTL, NTS)                                                                                  \
+    for (int g : {1024, 2048, 4096, 8192, 16384}) {                                                     \
+        float ms = time_ms([&] { v_static<K, U, NTL, NTS><<<g, 256>>>(src, ld, n, master, mom, op, src); }, reps); \
+        printf("static U=%d ntl=%d nts=%d grid %5d: %.3f ms  %.0f GB/s\n", U, NTL, NTS, g, ms, bytes / ms / 1e6); \
+    }
+    RUN(1, false, false)
+    RUN(2, false, false)
+    RUN(1, false, true)
+    RUN(1, true, true)
+    RUN(2, true, true)
+    RUN(1, true, false)
+    return 0;
+}
