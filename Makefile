@@ -25,3 +25,10 @@ build/%.s: gym_amd/csrc/%.hip
 
 clean:
 	rm -rf build $(LIB)
+
+# Diagnostic build with per-phase s_memtime stamps in the DeMo kernels (tools/demo_stamps.py).
+STAMP_LIB := build/libgym_amd_stamps.so
+stamps: $(STAMP_LIB)
+$(STAMP_LIB): $(SRC) gym_amd/csrc/ga_common.h include/gym_amd.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DGA_DEMO_STAMPS -shared -o $@ $(SRC)

@@ -172,11 +172,19 @@ def bench_diloco(args, coll, dev):
     else:  # sharded: read the reduce-scattered sum shard, master, mom; write master, mom, param shard
         alg_bytes = 6 * per * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic_diloco.json")
+    if coll.world == 1 and os.path.exists(tfile):
+        # HBM bytes per launch from the committed rocprofv3 PMC passes of this
+        # same configuration (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950)
+        t = json.load(open(tfile))
+        if t.get("algorithmic_bytes_per_launch") == alg_bytes:
+            traffic = t["traffic_bytes_per_launch"]
     out = {
         "ms_per_step": t * 1e3, "value": value, "K_total": K_total, "n_params": n_params,
         "kernel_ms": kern_ms, "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "ga_diloco_outer", "bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4)},
     }
     if coll.world > 1:

@@ -20,6 +20,21 @@
 
 namespace ga {
 
+// Diagnostic build only (tools/demo_stamps.py, -DGA_DEMO_STAMPS): s_memtime at
+// phase boundaries, one row of 16 per workgroup, into a buffer nothing else reads.
+#ifdef GA_DEMO_STAMPS
+__device__ unsigned long long* g_demo_stamps;
+#define GA_STAMP(i)                                                                              \
+    do {                                                                                         \
+        if (threadIdx.x == 0)                                                                    \
+            g_demo_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define GA_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
 constexpr int kDmBlock = 256;
 constexpr int kLd = 65;
 constexpr int kTile = 64 * kLd;
@@ -145,33 +160,136 @@ __device__ __forceinline__ ChunkIO chunk_io(const ga_demo_tensor& td, int c, int
 }
 
 constexpr int kCandMax = 1024;   // candidate list of the threshold top-k
-constexpr int kEntMax = 2048;    // entries per chunk supported by the residual (topk <= 2048)
-constexpr int kStage = 32;       // entries staged per residual pass
+constexpr int kEntMax = 512;     // entries per chunk (topk <= 512; the list lives in the candidate buffer)
+
+// r[i][c] += sum_e v_e * B1[b_e, row(i)] * B2[d_e, col0 + c] over an entry list
+// (the sparse form of B1^T . S . B2).  B2 rows come from the LDS copy BT of the
+// basis-2 table; B1 is the identity (n1 == 1), the same LDS table, or global.
+// Entries are processed in batches of 32: U[e][h] = v_e * B1[b_e, h] and the
+// B2 row offsets are staged in LDS (scratch: 32*64 + 32 words), then every
+// lane accumulates its 16 outputs with broadcast / 16-byte LDS reads.
+constexpr int kUBatch = 32;
+
+__device__ __forceinline__ void sparse_rank_update(float (&r)[4][4], const int* ent_bd, const float* ent_v, int E,
+                                                   const float* BT, const float* B1g, int b1mode,
+                                                   const ChunkIO& io, float* scratch) {
+    float* U = scratch;                                   // [kUBatch][64]
+    int* doff = reinterpret_cast<int*>(scratch + kUBatch * 64);  // [kUBatch] row offsets into BT (float4 units)
+    const int lane16 = threadIdx.x & 15;
+    for (int e0 = 0; e0 < E; e0 += kUBatch) {
+        const int ne = (E - e0) < kUBatch ? (E - e0) : kUBatch;
+        __syncthreads();  // previous batch consumed
+        for (int f = threadIdx.x; f < ne * 64; f += kDmBlock) {
+            const int e = f >> 6, h = f & 63;
+            const int bd = ent_bd[e0 + e];
+            const int b = bd >> 8;
+            const float v = ent_v[e0 + e];
+            float b1;
+            if (b1mode == 0) b1 = (h == b) ? 1.f : 0.f;
+            else if (b1mode == 1) b1 = BT[b * 64 + h];
+            else b1 = B1g[b * 64 + h];
+            U[f] = v * b1;
+            if (h == 0) doff[e] = (bd & 255) * 16;
+        }
+        __syncthreads();
+        const float4* BT4 = reinterpret_cast<const float4*>(BT);
+#pragma unroll 4
+        for (int e = 0; e < ne; ++e) {
+            const float4 wv = BT4[doff[e] + lane16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float u = U[e * 64 + io.row(i)];
+                r[i][0] = fmaf(u, wv.x, r[i][0]);
+                r[i][1] = fmaf(u, wv.y, r[i][1]);
+                r[i][2] = fmaf(u, wv.z, r[i][2]);
+                r[i][3] = fmaf(u, wv.w, r[i][3]);
+            }
+        }
+    }
+}
+
+// The basis-2 table of a chunk into LDS: issue (registers) ...
+struct TableStage {
+    float4 v[4];
+    __device__ __forceinline__ void issue(const float* tab) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = reinterpret_cast<const float4*>(tab)[threadIdx.x + 256 * i];
+    }
+    // ... and land (LDS), later, so the loads fly under other work.
+    __device__ __forceinline__ void land(float* lds) const {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) reinterpret_cast<float4*>(lds)[threadIdx.x + 256 * i] = v[i];
+    }
+};
+
+__device__ __forceinline__ int b1_mode(const ga_demo_tensor& td) {
+    return td.n1 == 1 ? 0 : (td.basis1 == td.basis2 ? 1 : 2);
+}
+
+// Bitonic compare-exchange stage over 64*R values held as v[r] = element
+// r*64 + lane of a sequence being sorted ascending (`size`, `stride` as in
+// the textbook network; element e sorts ascending iff (e & size) == 0).
+template <int R>
+__device__ __forceinline__ void bitonic_stage(uint32_t (&v)[R], int e_base, int size, int stride) {
+    const int lane = threadIdx.x & 63;
+    if (stride >= 64) {
+        const int rs = stride >> 6;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int r2 = r ^ rs;
+            if (r2 > r) {
+                const bool asc = (((e_base + r * 64) & size) == 0);
+                const uint32_t a = v[r], b = v[r2];
+                v[r] = asc ? (a < b ? a : b) : (a > b ? a : b);
+                v[r2] = asc ? (a > b ? a : b) : (a < b ? a : b);
+            }
+        }
+    } else {
+        const bool lower = (lane & stride) == 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t o = __shfl_xor(v[r], stride, 64);
+            const bool asc = (((e_base + r * 64 + lane) & size) == 0);
+            v[r] = (lower == asc) ? (v[r] < o ? v[r] : o) : (v[r] > o ? v[r] : o);
+        }
+    }
+}
 
 // Selection bits (T-map: lane t owns coefficients 16t .. 16t+15 of the padded
 // row-major grid) of the k largest keys; ties at the k-th key -> lowest index.
-// Fast path: T0 = the k-th largest of the 256 per-lane maxima is a lower bound
-// on the k-th largest key (>= k lanes hold a key >= T0), so the answer lies
-// among the keys >= T0; they are ranked exactly in LDS.  Falls back to a
-// 4-round 8-bit radix select when k > 256 or there are too many candidates
-// (e.g. an all-zero chunk, where every key ties).
+// Fast path (k <= 64): T0 = the k-th largest of the 256 per-lane maxima — a
+// lower bound on the k-th largest key, since >= k lanes hold a key >= T0 — by
+// a bitonic sort (each wave sorts its 64 maxima in registers, wave 0 merges
+// the four runs); the answer lies among the keys >= T0 (about k of them on
+// DCT coefficients), which are ranked exactly in LDS.  Falls back to a
+// 4-round 8-bit radix select when k > 64 or the candidates overflow (e.g. an
+// all-zero chunk, where every key ties).
 __device__ uint32_t select_topk(const uint32_t (&key)[16], int k, uint32_t* tmax, uint32_t* cand_key,
                                 uint8_t* cand_sel, int* hist, int* misc) {
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     uint32_t mymax = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) mymax = key[j] > mymax ? key[j] : mymax;
-    bool fast = k <= kDmBlock;
+    bool fast = k <= 64;
     uint32_t sel = 0;
     if (fast) {
-        tmax[t] = mymax;
+        // sizes 2..64: every wave sorts its maxima (run w ascending iff w even)
+        uint32_t v1[1] = {mymax};
+        for (int size = 2; size <= 64; size <<= 1)
+            for (int stride = size >> 1; stride > 0; stride >>= 1) bitonic_stage<1>(v1, wid * 64, size, stride);
+        tmax[t] = v1[0];
         __syncthreads();
-        int r = 0;
-        for (int j = 0; j < kDmBlock; ++j) {
-            const uint32_t o = tmax[j];
-            r += (o > mymax) | ((o == mymax) & (j < t));
+        if (wid == 0) {  // sizes 128, 256: merge the four runs
+            uint32_t v4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v4[r] = tmax[r * 64 + lane];
+            for (int size = 128; size <= 256; size <<= 1)
+                for (int stride = size >> 1; stride > 0; stride >>= 1) bitonic_stage<4>(v4, 0, size, stride);
+            const int e = 256 - k;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (r == (e >> 6) && lane == (e & 63)) misc[1] = (int)v4[r];
         }
-        if (r == k - 1) misc[1] = (int)mymax;
         __syncthreads();
         uint32_t T0 = (uint32_t)misc[1];
         if (T0 == 0u) T0 = 1u;  // key 0 marks padding; small chunks rank all their keys
@@ -261,10 +379,10 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ F,
     const float* __restrict__ B, T* param, const T* __restrict__ grad, T* delta, int64_t ld, float lr,
     float decay, float wd_factor, int32_t* payload, int64_t pstride, int64_t M, int ptr_vec) {
-    __shared__ float X[kTile];   // delta chunk (MFMA A operand); then the entry list
-    __shared__ float Y[kTile];   // T = X.F2, Y = F1^T.T; then the residual staging
+    __shared__ __attribute__((aligned(16))) float X[kTile];  // delta chunk (MFMA A operand); then the B2 table
+    __shared__ float Y[kTile];   // T = X.F2, Y = F1^T.T
     __shared__ uint32_t tmax[kDmBlock];
-    __shared__ uint32_t cand_key[kCandMax];
+    __shared__ uint32_t cand_key[kCandMax];  // candidates; then the entry list
     __shared__ uint8_t cand_sel[kCandMax];
     __shared__ int hist[256];
     __shared__ int misc[8];
@@ -280,6 +398,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
     payload += rep * pstride;
     const ChunkIO io = chunk_io<T>(td, c, ld, ptr_vec != 0);
     const int n1 = td.n1, n2 = td.n2, k = td.k;
+    GA_STAMP(0);
 
     // 1. error feedback in registers: x = decay*delta + lr*grad (+ decoupled weight decay on p)
     float x[4][4];
@@ -306,15 +425,21 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
         for (int e = 0; e < 4; ++e) X[io.row(i) * kLd + io.col0() + e] = (io.col0() + e < n2) ? x[i][e] : 0.f;
     }
     __syncthreads();
+    GA_STAMP(1);
 
     // 2. Y = F1^T . X . F2 on the matrix cores
     f32x16 acc = mm64<true, false>(X, F + (int64_t)td.basis2 * 4096);
     store_acc(Y, acc);
     __syncthreads();
+    GA_STAMP(2);
+    TableStage bt;
+    bt.issue(B + (int64_t)td.basis2 * 4096);  // lands in X (free now) after the product
     acc = mm64<false, true>(F + (int64_t)td.basis1 * 4096, Y);
     __syncthreads();
     store_acc(Y, acc);
+    bt.land(X);
     __syncthreads();
+    GA_STAMP(3);
 
     // 3. top-k of |Y| over the valid n1 x n2 coefficients
     const int row = threadIdx.x >> 2, col0 = 16 * (threadIdx.x & 3);
@@ -325,10 +450,11 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
         key[j] = valid ? (__float_as_uint(Y[row * kLd + col0 + j]) & 0x7fffffffu) + 1u : 0u;
     }
     const uint32_t sel = select_topk(key, k, tmax, cand_key, cand_sel, hist, misc);
+    GA_STAMP(4);
 
     // 4. emit the entries in ascending coefficient order; keep (b, d, v) in LDS
-    int* ent_bd = reinterpret_cast<int*>(X);
-    float* ent_v = X + kEntMax;
+    int* ent_bd = reinterpret_cast<int*>(cand_key);
+    float* ent_v = reinterpret_cast<float*>(cand_key + kEntMax);
     int slot = scan256(__popc(sel), misc + 4, nullptr);
     int32_t* out_idx = payload + td.payload_off + (int64_t)c * k;
     float* out_val = reinterpret_cast<float*>(payload + M) + td.payload_off + (int64_t)c * k;
@@ -344,6 +470,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
         }
     }
     __syncthreads();
+    GA_STAMP(5);
 
     // 5. residual: delta = x - sum_e v_e * outer(B1[b_e, :], B2[d_e, :])  (the sparse
     //    form of B1^T . S . B2: k rank-1 terms instead of two dense products)
@@ -352,32 +479,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) r[i][e] = 0.f;
-    const float* B1 = B + (int64_t)td.basis1 * 4096;
-    const float* B2 = B + (int64_t)td.basis2 * 4096;
-    float* U = Y;                 // [kStage][64]: v_e * B1[b_e, h]
-    float* W = Y + kStage * 64;   // [kStage][64]: B2[d_e, w]
-    for (int e0 = 0; e0 < k; e0 += kStage) {
-        const int ne = (k - e0) < kStage ? (k - e0) : kStage;
-        for (int f = threadIdx.x; f < ne * 128; f += kDmBlock) {
-            const int e = f >> 7, cidx = f & 127;
-            const int bd = ent_bd[e0 + e];
-            if (cidx < 64) U[e * 64 + cidx] = ent_v[e0 + e] * B1[(bd >> 8) * 64 + cidx];
-            else W[e * 64 + cidx - 64] = B2[(bd & 255) * 64 + cidx - 64];
-        }
-        __syncthreads();
-        for (int e = 0; e < ne; ++e) {
-            const float4 wv = *reinterpret_cast<const float4*>(W + e * 64 + io.col0());
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float u = U[e * 64 + io.row(i)];
-                r[i][0] = fmaf(u, wv.x, r[i][0]);
-                r[i][1] = fmaf(u, wv.y, r[i][1]);
-                r[i][2] = fmaf(u, wv.z, r[i][2]);
-                r[i][3] = fmaf(u, wv.w, r[i][3]);
-            }
-        }
-        __syncthreads();
-    }
+    sparse_rank_update(r, ent_bd, ent_v, k, X, B + (int64_t)td.basis1 * 4096, b1_mode(td), io, Y);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (io.live(i)) {
@@ -387,6 +489,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
             store4(delta, io, i, o);
         }
     }
+    GA_STAMP(6);
 }
 
 template <typename T>
@@ -394,8 +497,8 @@ __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ B,
     const int32_t* __restrict__ payload, int64_t pstride, int64_t M, int64_t nsrc, T* param, T* grad,
     int64_t K, int64_t ld, float lr, int ptr_vec) {
-    __shared__ float S[kTile];
-    __shared__ int cnt[4096];
+    __shared__ float S[kTile];      // scatter-mean tile (row stride kLd), then the decoded g
+    __shared__ uint16_t cnt[4096];  // hits per coefficient
     __shared__ int misc[4];
 
     const int chunk = blockIdx.x;
@@ -426,11 +529,13 @@ __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
         }
         __syncthreads();
     }
-    for (int e = threadIdx.x; e < 4096; e += kDmBlock) {
-        const int n = cnt[e];
-        if (n > 1) S[(e >> 6) * kLd + (e & 63)] /= (float)n;
+    if (nsrc > 1) {
+        for (int e = threadIdx.x; e < 4096; e += kDmBlock) {
+            const int n = cnt[e];
+            if (n > 1) S[(e >> 6) * kLd + (e & 63)] /= (float)n;
+        }
+        __syncthreads();
     }
-    __syncthreads();
 
     // g = B1^T . S . B2 on the matrix cores, staged back through LDS for row-major I/O
     f32x16 acc = mm64<true, false>(S, B + (int64_t)td.basis2 * 4096);
@@ -474,6 +579,12 @@ static int check_tensors_host(int32_t ntensors, int32_t nchunks) {
 using namespace ga;
 
 extern "C" GA_API int ga_demo_tensor_bytes(void) { return (int)sizeof(ga_demo_tensor); }
+
+#ifdef GA_DEMO_STAMPS
+extern "C" GA_API int ga_demo_stamps_set(unsigned long long* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(ga::g_demo_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 extern "C" GA_API int ga_demo_encode(int dtype, const ga_demo_tensor* tensors, int32_t ntensors, int32_t nchunks,
                                      const float* F, const float* B, void* param, const void* grad, void* delta,

@@ -91,8 +91,8 @@ class DemoPlan:
                     sizes.append(n)
             gy, gx = R // n1, C // n2
             k = max(1, min(self.topk, n1 * n2))
-            if k > 2048:
-                raise NotImplementedError("DeMo: more than 2048 entries per chunk (compression_topk <= 2048)")
+            if k > 512:
+                raise NotImplementedError("DeMo: more than 512 entries per chunk (compression_topk <= 512)")
             d = DemoTensor(offset=off, payload_off=payload_off, rows=R, cols=C, n1=n1, n2=n2, gy=gy, gx=gx, k=k,
                            basis1=basis_of[n1], basis2=basis_of[n2], chunk_start=chunk_start)
             descs.append(d)

@@ -283,7 +283,7 @@ def _payload_host(pl, plan):
     return a[:, : plan.M], a[:, plan.M: 2 * plan.M].view(np.float32)
 
 
-@pytest.mark.parametrize("K", [1, 2, 3])
+@pytest.mark.parametrize("K", [1, 2, 3, 5])
 def test_demo_encode_decode_matches_oracle(K):
     from gym_amd import ops
     shapes = DEMO_SHAPES

@@ -1,0 +1,71 @@
+"""Per-phase cycle shares of ga_demo_encode (diagnostic build, make stamps).
+
+Loads build/libgym_amd_stamps.so (same kernels + s_memtime stamps at phase
+boundaries), runs the encode of GPT-2 350M once, and prints the median
+cycles each workgroup spent per phase.  Read the shares, not the absolute
+time (the stamps themselves perturb the kernel)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from gym_amd import _lib  # noqa: E402
+from gym_amd.arena import ArenaLayout  # noqa: E402
+from gym_amd.demo_codec import DemoPlan  # noqa: E402
+from gym_amd.shapes import MODELS  # noqa: E402
+
+PHASES = ["load+error-feedback", "DCT product 1", "DCT product 2", "top-k select", "emit entries", "residual+store"]
+
+
+def main():
+    model = sys.argv[1] if len(sys.argv) > 1 else "gpt2-350m"
+    L = ctypes.CDLL(os.path.join(ROOT, "build", "libgym_amd_stamps.so"))
+    for name, (res, args) in _lib.SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    L.ga_demo_stamps_set.argtypes = [ctypes.c_void_p]
+    dev = torch.device("cuda:0")
+    layout = ArenaLayout(MODELS[model]())
+    plan = DemoPlan(layout).to(dev)
+    P = torch.randn(layout.n, device=dev) * 0.02
+    G = torch.randn(layout.n, device=dev) * 1e-3
+    D = torch.zeros(layout.n, device=dev)
+    pl = torch.zeros(2 * plan.M, dtype=torch.int32, device=dev)
+    stamps = torch.zeros(plan.nchunks * 16, dtype=torch.int64, device=dev)
+    assert L.ga_demo_stamps_set(ctypes.c_void_p(stamps.data_ptr())) == 0
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def run():
+        rc = L.ga_demo_encode(0, ctypes.c_void_p(plan.desc.data_ptr()), plan.ntensors, plan.nchunks,
+                              ctypes.c_void_p(plan.F.data_ptr()), ctypes.c_void_p(plan.B.data_ptr()),
+                              ctypes.c_void_p(P.data_ptr()), ctypes.c_void_p(G.data_ptr()),
+                              ctypes.c_void_p(D.data_ptr()), 1, layout.n, 1e-3, 0.999, 1.0,
+                              ctypes.c_void_p(pl.data_ptr()), 2 * plan.M, plan.M, s)
+        assert rc == 0, L.ga_last_error()
+
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    run()
+    e1.record()
+    torch.cuda.synchronize()
+    st = stamps.view(-1, 16).cpu().numpy()[:, :7].astype(np.int64)
+    d = np.diff(st, axis=1)
+    tot = st[:, 6] - st[:, 0]
+    print(f"{model}: {plan.nchunks} chunks, kernel {e0.elapsed_time(e1):.3f} ms (stamped build)")
+    print(f"workgroup lifetime cycles: median {np.median(tot):.0f}  p90 {np.percentile(tot, 90):.0f}")
+    for i, name in enumerate(PHASES):
+        print(f"  {name:22s} median {np.median(d[:, i]):8.0f} cyc  share {np.median(d[:, i]) / np.median(tot):6.1%}")
+    stg = stamps.view(-1, 16).cpu().numpy()[:, 7].astype(np.int64) - st[:, 5]
+    print(f"  (residual: staging of the first {32} entries median {np.median(stg):.0f} cyc)")
+
+
+if __name__ == "__main__":
+    main()

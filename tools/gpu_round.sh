@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel stats, PMC traffic passes.
+# Usage (via gpurun): bash tools/gpu_round.sh <tag>
+set -o pipefail
+TAG=${1:-r01}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 500 python -m pytest tests -m gpu -x -q > $O/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -30 $O/gpu_tests.log; exit 1; }
+tail -2 $O/gpu_tests.log
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1 || { echo "PROF FAILED"; tail -20 $O/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 bench.py --no-extras --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -20 $O/pmc_fetch.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 bench.py --no-extras --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -20 $O/pmc_write.log; exit 1; }
+echo DONE
