@@ -50,6 +50,11 @@ XGMI_LINK_GBS = 153.0      # per xGMI link (SURVEY §8(d) roofline model)
 def setup_dist(gpus):
     if gpus > 1 or "RANK" in os.environ:
         local = int(os.environ.get("LOCAL_RANK", 0))
+        if os.environ.get("GA_BENCH_BACKEND") == "gloo":
+            # rehearsal of the multi-rank path on a 1-GPU box: ranks share the GPUs over gloo
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+            return Collective()
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     else:
@@ -169,17 +174,19 @@ def bench_diloco(args, coll, dev):
     per = eng.per
     if coll.world == 1:  # read every replica, master, mom; write master, mom, every replica
         alg_bytes = (2 * K + 4) * per * 4
-    else:  # sharded: read the reduce-scattered sum shard, master, mom; write master, mom, param shard
+    elif eng.shard:  # RCCL: read the reduce-scattered sum shard, master, mom; write master, mom, param shard
         alg_bytes = 6 * per * 4
+    else:  # gloo rehearsal: read the all-reduced sum, master, mom; write master, mom, every replica
+        alg_bytes = (5 + K) * per * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic_diloco.json")
     if coll.world == 1 and os.path.exists(tfile):
         # HBM bytes per launch from the committed rocprofv3 PMC passes of this
         # same configuration (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950)
-        t = json.load(open(tfile))
-        if t.get("algorithmic_bytes_per_launch") == alg_bytes:
-            traffic = t["traffic_bytes_per_launch"]
+        pmc = json.load(open(tfile))
+        if pmc.get("algorithmic_bytes_per_launch") == alg_bytes:
+            traffic = pmc["traffic_bytes_per_launch"]
     out = {
         "ms_per_step": t * 1e3, "value": value, "K_total": K_total, "n_params": n_params,
         "kernel_ms": kern_ms, "roofline": {
@@ -210,10 +217,14 @@ def bench_sparta(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
 
     t = timed_loop(step, args.steps, args.warmup, coll)
     eng.check()
+    # the number selected (untimed; the fused single-GPU pass produces no list)
+    ops.sparta_select(rs.data, layout.n, eng.cap, eng.idx, eng.vals, eng.count, eng.work, seed=42, iteration=0, p=p)
     M = int(eng.count[0].item())
-    alg = 2 * 4 * K * M + 4 * M * 2  # gather K replicas + scatter K replicas + idx write/read
+    alg = 2 * 4 * K * M + (8 * M if coll.world > 1 else 0)  # K-replica gather + write-back (+ idx/vals list)
     return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
-            "K_local": K, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1)}
+            "K_local": K, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1),
+            "path": "fused select+gather+average+write-back" if coll.world == 1 else
+                    "select+gather, RCCL all-reduce of packed values, scatter"}
 
 
 def bench_simple(args, coll, dev, K=8, model="gpt2-char"):

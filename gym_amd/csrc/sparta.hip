@@ -163,27 +163,32 @@ __global__ __launch_bounds__(kScanBlock) void sparta_scan_kernel(const int32_t* 
 // ascending replica order.
 constexpr int kGatherSlots = 2048;  // floats of LDS for the (element, replica) values
 
+// With divisor > 0 the kernel also finishes the step for a single process
+// (ga_sparta_average_local): each selected element's average is written back
+// to every replica right after its gather, while its lines are still in L2
+// (full-line write-backs instead of partial writes from a later scatter pass).
 template <typename T>
 __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t n, const int32_t* tile_offsets,
-                                                                 const T* __restrict__ src, int64_t K, int64_t ld,
+                                                                 T* src, int64_t K, int64_t ld,
                                                                  int64_t cap, int32_t* __restrict__ idx,
-                                                                 T* __restrict__ vals) {
+                                                                 T* __restrict__ vals, float divisor) {
     __shared__ int wave_tot[4];
     __shared__ int32_t sel_list[kSpTile];
     __shared__ float gv[kGatherSlots];
+    __shared__ float gavg[kSpBlock];
     const int64_t tile0 = (int64_t)blockIdx.x * kSpTile;
     const int64_t e0 = tile0 + (int64_t)threadIdx.x * kSpPerThread;
     uint32_t bits = e0 < n ? pred_bits16(P, e0, n) : 0u;
     int total;
     int local = block_excl_scan_256(__popc(bits), wave_tot, &total);
-    const int64_t out0 = tile_offsets[blockIdx.x];
+    const int64_t out0 = tile_offsets ? tile_offsets[blockIdx.x] : 0;
     while (bits) {
         const int j = __ffs(bits) - 1;
         bits &= bits - 1;
         const int32_t i = (int32_t)(threadIdx.x * kSpPerThread + j);
         sel_list[local] = i;
         const int64_t pos = out0 + local;
-        if (pos < cap) idx[pos] = (int32_t)(tile0 + i);
+        if (idx && pos < cap) idx[pos] = (int32_t)(tile0 + i);
         ++local;
     }
     __syncthreads();
@@ -192,26 +197,40 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
     for (int c0 = 0; c0 < total; c0 += per_pass) {
         const int ce = (total - c0) < per_pass ? (total - c0) : per_pass;
         if (K <= kGatherSlots) {
+            // replica-major lanes: consecutive lanes read consecutive selected
+            // elements of ONE replica (same 16 KB tile -> few DRAM pages)
             const int Ki = (int)K;
             for (int f = threadIdx.x; f < ce * Ki; f += kSpBlock) {
-                const int e = f / Ki, k = f - e * Ki;
-                gv[f] = Elem<T>::load(src + (int64_t)k * ld + tile0 + sel_list[c0 + e]);
+                const int k = f / ce, e = f - k * ce;
+                gv[e * Ki + k] = Elem<T>::load(src + (int64_t)k * ld + tile0 + sel_list[c0 + e]);
             }
             __syncthreads();
             if (threadIdx.x < ce) {
                 float acc = 0.f;
                 for (int64_t k = 0; k < K; ++k) acc += gv[threadIdx.x * K + k];
                 const int64_t pos = out0 + c0 + threadIdx.x;
-                if (pos < cap) Elem<T>::store(vals + pos, acc);
+                if (vals && pos < cap) Elem<T>::store(vals + pos, acc);
+                if (divisor > 0.f) gavg[threadIdx.x] = acc / divisor;
             }
             __syncthreads();
+            if (divisor > 0.f) {
+                for (int f = threadIdx.x; f < ce * Ki; f += kSpBlock) {
+                    const int k = f / ce, e = f - k * ce;
+                    Elem<T>::store(src + (int64_t)k * ld + tile0 + sel_list[c0 + e], gavg[e]);
+                }
+                __syncthreads();
+            }
         } else {  // very many replicas: one element at a time, lanes over replicas
             const int64_t i = tile0 + sel_list[c0];
             float acc = 0.f;
             if (threadIdx.x == 0)
                 for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + k * ld + i);
             const int64_t pos = out0 + c0;
-            if (threadIdx.x == 0 && pos < cap) Elem<T>::store(vals + pos, acc);
+            if (threadIdx.x == 0 && vals && pos < cap) Elem<T>::store(vals + pos, acc);
+            if (threadIdx.x == 0 && divisor > 0.f) {
+                const float a = acc / divisor;
+                for (int64_t k = 0; k < K; ++k) Elem<T>::store(src + k * ld + i, a);
+            }
         }
     }
 }
@@ -236,17 +255,21 @@ static int64_t sparta_tiles(int64_t n) { return ceil_div(n, kSpTile); }
 
 template <typename T>
 static int launch_select(const void* src, int64_t K, int64_t ld, int64_t n, const Pred& P, int64_t cap,
-                         int32_t* idx, void* vals, int64_t* count, void* work, hipStream_t stream) {
+                         int32_t* idx, void* vals, int64_t* count, void* work, float divisor, hipStream_t stream) {
     const int64_t ntiles = sparta_tiles(n);
-    int32_t* tile_counts = (int32_t*)work;
-    int32_t* tile_offsets = tile_counts + ntiles;
-    hipLaunchKernelGGL(sparta_count_kernel, dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n, tile_counts);
-    if (int e = check_launch("ga_sparta_select(count)")) return e;
-    hipLaunchKernelGGL(sparta_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream, tile_counts, ntiles, tile_offsets,
-                       cap, count);
-    if (int e = check_launch("ga_sparta_select(scan)")) return e;
+    int32_t* tile_offsets = nullptr;
+    if (idx || vals || count) {  // positions of the packed list: count + scan passes
+        int32_t* tile_counts = (int32_t*)work;
+        tile_offsets = tile_counts + ntiles;
+        hipLaunchKernelGGL(sparta_count_kernel, dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
+                           tile_counts);
+        if (int e = check_launch("ga_sparta_select(count)")) return e;
+        hipLaunchKernelGGL(sparta_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream, tile_counts, ntiles,
+                           tile_offsets, cap, count);
+        if (int e = check_launch("ga_sparta_select(scan)")) return e;
+    }
     hipLaunchKernelGGL((sparta_select_kernel<T>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
-                       tile_offsets, (const T*)src, K, ld, cap, idx, (T*)vals);
+                       tile_offsets, (T*)src, K, ld, cap, idx, (T*)vals, divisor);
     return check_launch("ga_sparta_select(gather)");
 }
 
@@ -287,9 +310,39 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     P.it_hi = (uint32_t)(iteration >> 32);
     P.thr = threshold;
     switch (dtype) {
-        case GA_F32: return launch_select<float>(src, K, ld, n, P, cap, idx, vals, count, work, stream);
-        case GA_BF16: return launch_select<__hip_bfloat16>(src, K, ld, n, P, cap, idx, vals, count, work, stream);
+        case GA_F32: return launch_select<float>(src, K, ld, n, P, cap, idx, vals, count, work, 0.f, stream);
+        case GA_BF16:
+            return launch_select<__hip_bfloat16>(src, K, ld, n, P, cap, idx, vals, count, work, 0.f, stream);
         default: set_error("ga_sparta_select: unknown dtype %d", dtype); return GA_EINVAL;
+    }
+}
+
+extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
+                                              const uint8_t* mask, uint64_t seed, uint64_t iteration,
+                                              uint32_t threshold, float divisor, int32_t* idx, void* vals,
+                                              int64_t cap, int64_t* count, void* work, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "ga_sparta_average_local: n=%lld out of range", (long long)n);
+    GA_REQUIRE(K >= 1 && cap >= 0, "ga_sparta_average_local: bad K/cap");
+    GA_REQUIRE(divisor > 0.0f, "ga_sparta_average_local: divisor must be > 0");
+    GA_REQUIRE(K == 1 || ld >= n, "ga_sparta_average_local: ld < n");
+    GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_average_local: threshold > 2^24");
+    GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_average_local: mask alignment");
+    GA_REQUIRE((idx == nullptr && vals == nullptr && count == nullptr) || (idx && vals && count && work),
+               "ga_sparta_average_local: idx, vals, count and work go together");
+    if (n == 0) return GA_OK;
+    GA_REQUIRE(reps, "ga_sparta_average_local: null replicas");
+    Pred P;
+    P.mask = mask;
+    P.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+    P.it_lo = (uint32_t)iteration;
+    P.it_hi = (uint32_t)(iteration >> 32);
+    P.thr = threshold;
+    switch (dtype) {
+        case GA_F32: return launch_select<float>(reps, K, ld, n, P, cap, idx, vals, count, work, divisor, stream);
+        case GA_BF16:
+            return launch_select<__hip_bfloat16>(reps, K, ld, n, P, cap, idx, vals, count, work, divisor, stream);
+        default: set_error("ga_sparta_average_local: unknown dtype %d", dtype); return GA_EINVAL;
     }
 }
 

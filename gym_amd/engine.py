@@ -161,6 +161,10 @@ class Sparta:
         else:
             self.check()
             cap_used = self.cap
+        if self.coll.world == 1:  # every node is a local replica: one fused pass, no exchange
+            ops.sparta_average_local(reps, n, float(self.K_total), mask=mask, seed=seed, iteration=iteration,
+                                     p=self.p)
+            return
         ops.sparta_select(reps, n, cap_used, self.idx, self.vals, self.count, self.work, mask=mask, seed=seed,
                           iteration=iteration, p=self.p)
         self.coll.all_reduce_(self.vals[:cap_used])

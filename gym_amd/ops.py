@@ -125,6 +125,27 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
                                  _p(work), _stream()), "ga_sparta_select")
 
 
+def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0, idx=None, vals=None, cap=0,
+                         count=None, work=None):
+    """Single-process SPARTA step over [K, ld] replicas: selected elements of
+    every replica <- (sum over replicas) / divisor, one pass (optional packed
+    idx/vals/count outputs as sparta_select)."""
+    r2 = _as2d(reps)
+    _gpu(r2, mask, idx, vals, count, work)
+    K, ld = _rows_ld(r2)
+    if mask is not None and (mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n):
+        raise ValueError("sparta_average_local: mask must be uint8/bool with >= n elements")
+    if idx is not None:
+        if idx.dtype != torch.int32 or vals.dtype != r2.dtype or count.dtype != torch.int64:
+            raise TypeError("sparta_average_local: idx int32, vals arena dtype, count int64")
+        if idx.numel() < cap or vals.numel() < cap or work.numel() < lib().ga_sparta_workspace_bytes(int(n)):
+            raise ValueError("sparta_average_local: output buffers too small")
+    thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
+    check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, int(n), _p(mask), int(seed) & (2**64 - 1),
+                                        int(iteration) & (2**64 - 1), thr, float(divisor), _p(idx), _p(vals),
+                                        int(cap), _p(count), _p(work), _stream()), "ga_sparta_average_local")
+
+
 def sparta_scatter(vals, idx, count, cap, divisor, dst):
     dst2 = _as2d(dst)
     _gpu(vals, idx, count, dst2)

@@ -130,6 +130,19 @@ GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
                              const int64_t* count, int64_t cap, float divisor,
                              void* dst, int64_t K, int64_t ld, hipStream_t stream);
 
+/*
+ * Single-process SPARTA step (every node is a local replica, no exchange):
+ * select as ga_sparta_select, then each selected element of every replica
+ * <- (sum over the K replicas) / divisor, in the same pass (the gathered lines
+ * are written back while still in L2).  idx/vals/count/work may all be null
+ * (no packed list, no count/scan pass); if given they are filled as by
+ * ga_sparta_select.  Replaces sparta.py:113-131 for batched replicas.
+ */
+GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
+                                   const uint8_t* mask, uint64_t seed, uint64_t iteration,
+                                   uint32_t threshold, float divisor, int32_t* idx, void* vals,
+                                   int64_t cap, int64_t* count, void* work, hipStream_t stream);
+
 /* ---- DeMo DCT codec ------------------------------------------------------ */
 
 /*

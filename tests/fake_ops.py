@@ -75,6 +75,15 @@ def sparta_scatter(vals, idx, count, cap, divisor, dst):
         d2[r, ii] = v
 
 
+def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0, idx=None, vals=None, cap=0,
+                         count=None, work=None):
+    m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p)
+    r2 = _2d(reps)
+    out = osparta.sparse_average(list(_np(r2)[:, :n]), m, divisor)
+    for k in range(r2.shape[0]):
+        r2[k, :n].copy_(torch.from_numpy(out[k]).to(r2.dtype))
+
+
 def _tensor_slices(plan):
     e = 0
     for shape, off, nel, ne in zip(plan.layout.shapes, plan.layout.offsets, plan.layout.numels,

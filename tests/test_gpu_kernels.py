@@ -209,6 +209,38 @@ def test_sparta_philox_select_gather_scatter(n, p, K):
         assert np.array_equal(got[k], want[k])
 
 
+@pytest.mark.parametrize("K,with_list,use_mask", [(32, False, False), (3, True, False), (2, False, True)])
+def test_sparta_average_local(K, with_list, use_mask):
+    """Fused single-process step: select + gather + average + write-back."""
+    from gym_amd import ops
+    n, p = 300_001, 0.01
+    rng = np.random.default_rng(K)
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    seed, it = 99, 4
+    if use_mask:
+        m = rng.random(n) < 0.02
+        mask_t = torch.zeros(n + 15, dtype=torch.uint8, device=DEV)
+        mask_t[:n] = torch.from_numpy(m.astype(np.uint8)).to(DEV)
+    else:
+        m = osparta.philox_mask(n, seed, it, p)
+        mask_t = None
+    src = t(x)
+    kw = {}
+    if with_list:
+        cap = int(m.sum()) + 16
+        idx, count, work = _sparta_buffers(n, cap)
+        vals = torch.empty(cap, device=DEV)
+        kw = dict(idx=idx, vals=vals, cap=cap, count=count, work=work)
+    ops.sparta_average_local(src, n, float(K), mask=mask_t, seed=seed, iteration=it, p=p, **kw)
+    want = osparta.sparse_average(list(x), m)
+    got = host(src)
+    for k in range(K):
+        assert np.array_equal(got[k], want[k])
+    if with_list:
+        c = int(count[0].item())
+        assert c == int(m.sum()) and np.array_equal(idx[:c].cpu().numpy(), np.flatnonzero(m))
+
+
 def test_sparta_overflow_flag():
     from gym_amd import ops
     n = 10_000

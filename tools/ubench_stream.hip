@@ -88,6 +88,7 @@ int main() {
     CK(hipMemset(src, 1, 4 * K * n)); CK(hipMemset(master, 1, 4 * n)); CK(hipMemset(mom, 1, 4 * n)); CK(hipMemset(big2, 1, 16 * n));
     const long nv = 4 * n / 4;  // copy 4*n floats = 2 GB read + 2 GB write
     int reps = 10;
+    if (getenv("ONLY_DILOCO")) goto diloco;
     for (int g : {256, 512, 1024, 2048, 4096}) {
         float ms = time_ms([&] { read_only<<<g, 256>>>((const float4*)src, out, 2 * nv); }, reps);
         printf("read-only 4GB       grid %5d: %.0f GB/s\n", g, 8.0 * 2 * n / ms / 1e6 * 2);
@@ -104,8 +105,9 @@ int main() {
         float ms = time_ms([&] { copy_chunk<4><<<g, 256>>>((const float4*)src, (float4*)big2, nv, chunk); }, reps);
         printf("copy chunk %6ld (grid %ld): %.0f GB/s\n", chunk, g, 2 * 16.0 * n / ms / 1e6);
     }
+diloco:
     const double bytes = (2.0 * K + 4.0) * 4.0 * n;
-    for (long chunk : {1024L, 2048L, 4096L, 8192L, 16384L}) {
+    for (long chunk : {128L, 256L, 512L, 1024L, 2048L}) {
         long g = (n / 4 + chunk - 1) / chunk;
         float ms = time_ms([&] { diloco_chunk<8, 1><<<g, 256>>>(src, n, n, master, mom, src, chunk); }, reps);
         float ms2 = time_ms([&] { diloco_chunk<8, 2><<<g, 256>>>(src, n, n, master, mom, src, chunk); }, reps);
