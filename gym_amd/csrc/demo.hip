@@ -2,20 +2,22 @@
 // update (ga_demo_encode) and the gathered scatter-mean + inverse DCT + sign-SGD
 // apply (ga_demo_decode).  One 256-lane workgroup (4 waves) per chunk.
 //
-// Every transform is a pair of 64x64x64 fp32 products on the matrix cores
-// (v_mfma_f32_32x32x2_f32: exact f32 FMA chains in k order, each wave owns one
-// 32x32 quadrant of the product).  Chunks with n1, n2 < 64 are computed zero
-// padded: the 64x64 basis tables are zero outside n x n, so padded rows and
-// columns of every product are exactly 0 and never selected.
+// Transforms run on the matrix cores as 64x64x64 fp32 products
+// (v_mfma_f32_32x32x2_f32: exact f32 FMA chains in k order; each wave owns one
+// 32x32 quadrant).  Chunks with n1, n2 < 64 are computed zero padded: the basis
+// tables are zero outside n x n, so padded rows/columns are exactly 0.
 //
-// LDS per workgroup: two 64x65 fp32 tiles (row stride 65 keeps the column reads
-// of the A operand conflict free) + a 256-bin histogram: ~34 KB.
+// LDS layout (per workgroup): ONE 64x65 working tile, products computed in
+// place (accumulate in registers, barrier, store back), and ONE copy of the
+// chunk's DCT basis F (spatial row i, frequency column k) with the same
+// 65-float row stride: every operand orientation the transforms need (F, F^T,
+// as A or B operand) then reads 32 consecutive lanes from 32 different banks.
+// Encode ~40 KB (4 workgroups per CU), decode ~37 KB.
 //
-// Top-k (demo.py:315-328, torch.topk(|x|, k, sorted=False)) is an exact radix
-// select on the |y| bit pattern (4 rounds of 8 bits) followed by an ordered
-// compaction; among coefficients tied with the k-th magnitude the lowest
-// coefficient index wins, and a chunk's entries are emitted in ascending index
-// order (the reference's order is unspecified; only the set matters).
+// Top-k (demo.py:315-328, torch.topk(|x|, k, sorted=False)): exact; among
+// coefficients tied with the k-th magnitude the lowest index wins, and a
+// chunk's entries are emitted in ascending index order (the reference's order
+// is unspecified; only the set matters).
 #include "ga_common.h"
 
 namespace ga {
@@ -41,11 +43,9 @@ constexpr int kTile = 64 * kLd;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// Quadrant of C = opA . Bm (64x64x64) for this wave.
-//   A_ROW_LDS: A[i][k] = A[i*kLd + k] (LDS tile); else A[i][k] = A[k*64 + i] (a
-//   transposed 64x64 global table: the F1^T / B1^T of the left transform).
-//   B_LDS:     B[k][j] = Bm[k*kLd + j] (LDS tile); else Bm[k*64 + j] (global table).
-template <bool A_ROW_LDS, bool B_LDS>
+// Quadrant of C = A . B (64x64x64) for this wave, operands addressed by
+// compile-time strides: A[i][k] = A[i*ASI + k*ASK], B[k][j] = B[k*BSK + j*BSJ].
+template <int ASI, int ASK, int BSK, int BSJ>
 __device__ __forceinline__ f32x16 mm64(const float* A, const float* Bm) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = 32 * (w >> 1) + (lane & 31);
@@ -57,12 +57,15 @@ __device__ __forceinline__ f32x16 mm64(const float* A, const float* Bm) {
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
         const int k = 2 * s + h;
-        const float a = A_ROW_LDS ? A[i * kLd + k] : A[k * 64 + i];
-        const float b = B_LDS ? Bm[k * kLd + j] : Bm[k * 64 + j];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[i * ASI + k * ASK], Bm[k * BSK + j * BSJ], acc, 0, 0, 0);
     }
     return acc;
 }
+
+// operand addressing modes
+#define TILE_ROW kLd, 1      // a 64x65 LDS tile, or the LDS basis F, read by rows
+#define TILE_COL 1, kLd      // the same, transposed (F^T)
+#define GTAB_COL 1, 64       // a 64x64 global table, transposed
 
 // Row of accumulator register r for this lane (C/D layout of the 32x32 MFMA).
 __device__ __forceinline__ int acc_row(int r) {
@@ -161,167 +164,165 @@ __device__ __forceinline__ ChunkIO chunk_io(const ga_demo_tensor& td, int c, int
 
 constexpr int kCandMax = 1024;   // candidate list of the threshold top-k
 constexpr int kEntMax = 512;     // entries per chunk (topk <= 512; the list lives in the candidate buffer)
+constexpr int kUBatch = 32;      // residual entries staged per pass
 
-// r[i][c] += sum_e v_e * B1[b_e, row(i)] * B2[d_e, col0 + c] over an entry list
-// (the sparse form of B1^T . S . B2).  B2 rows come from the LDS copy BT of the
-// basis-2 table; B1 is the identity (n1 == 1), the same LDS table, or global.
-// Entries are processed in batches of 32: U[e][h] = v_e * B1[b_e, h] and the
-// B2 row offsets are staged in LDS (scratch: 32*64 + 32 words), then every
-// lane accumulates its 16 outputs with broadcast / 16-byte LDS reads.
-constexpr int kUBatch = 32;
-
-__device__ __forceinline__ void sparse_rank_update(float (&r)[4][4], const int* ent_bd, const float* ent_v, int E,
-                                                   const float* BT, const float* B1g, int b1mode,
-                                                   const ChunkIO& io, float* scratch) {
-    float* U = scratch;                                   // [kUBatch][64]
-    int* doff = reinterpret_cast<int*>(scratch + kUBatch * 64);  // [kUBatch] row offsets into BT (float4 units)
-    const int lane16 = threadIdx.x & 15;
-    for (int e0 = 0; e0 < E; e0 += kUBatch) {
-        const int ne = (E - e0) < kUBatch ? (E - e0) : kUBatch;
-        __syncthreads();  // previous batch consumed
-        for (int f = threadIdx.x; f < ne * 64; f += kDmBlock) {
-            const int e = f >> 6, h = f & 63;
-            const int bd = ent_bd[e0 + e];
-            const int b = bd >> 8;
-            const float v = ent_v[e0 + e];
-            float b1;
-            if (b1mode == 0) b1 = (h == b) ? 1.f : 0.f;
-            else if (b1mode == 1) b1 = BT[b * 64 + h];
-            else b1 = B1g[b * 64 + h];
-            U[f] = v * b1;
-            if (h == 0) doff[e] = (bd & 255) * 16;
-        }
-        __syncthreads();
-        const float4* BT4 = reinterpret_cast<const float4*>(BT);
-#pragma unroll 4
-        for (int e = 0; e < ne; ++e) {
-            const float4 wv = BT4[doff[e] + lane16];
+// Stage a chunk's basis into LDS as F[i*kLd + k] (spatial i, frequency k).
+// From the DCT table F (row-major 64x64): a straight copy; from the inverse
+// table B = F^T: the transpose.  Global reads are row-major (coalesced); the
+// LDS writes of consecutive lanes land in different banks either way.
+template <bool FROM_B>
+__device__ __forceinline__ void stage_basis(float* FT, const float* tab) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float u = U[e * 64 + io.row(i)];
-                r[i][0] = fmaf(u, wv.x, r[i][0]);
-                r[i][1] = fmaf(u, wv.y, r[i][1]);
-                r[i][2] = fmaf(u, wv.z, r[i][2]);
-                r[i][3] = fmaf(u, wv.w, r[i][3]);
-            }
+    for (int r = 0; r < 4; ++r) {
+        const int q = threadIdx.x + 256 * r;  // float4 index of the global table
+        const float4 v = reinterpret_cast<const float4*>(tab)[q];
+        const int row = q >> 4, c0 = 4 * (q & 15);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (FROM_B) FT[(c0 + c) * kLd + row] = vv[c];  // B[row][c0+c] = F[c0+c][row]
+            else FT[row * kLd + c0 + c] = vv[c];
         }
     }
 }
 
-// The basis-2 table of a chunk into LDS: issue (registers) ...
-struct TableStage {
-    float4 v[4];
-    __device__ __forceinline__ void issue(const float* tab) {
+// r[i][c] -= sum_e v_e * B1[b_e, row(i)] * B2[d_e, col0 + c] over an entry list
+// (the sparse form of B1^T . S . B2, B = F^T).  Per batch of 32 entries,
+// U[e][h] = v_e * F1[h, b_e] and W[e][w] = F2[w, d_e] are staged in `scratch`
+// (2 x 32 x 64 floats); every lane then accumulates its 16 outputs from
+// broadcast and 16-byte LDS reads.  F1 is the identity (n1 == 1), the LDS
+// basis, or the global inverse table B1 (b1mode 0 / 1 / 2).
+__device__ __forceinline__ void sparse_rank_update(float (&r)[4][4], const int* ent_bd, const float* ent_v, int E,
+                                                   const float* FT, const float* B1g, int b1mode, const ChunkIO& io,
+                                                   float* scratch) {
+    float* U = scratch;
+    float* W = scratch + kUBatch * 64;
+    for (int e0 = 0; e0 < E; e0 += kUBatch) {
+        const int ne = (E - e0) < kUBatch ? (E - e0) : kUBatch;
+        __syncthreads();  // previous batch consumed
+        for (int f = threadIdx.x; f < ne * 128; f += kDmBlock) {
+            const int e = f >> 7, x = f & 127;
+            const int bd = ent_bd[e0 + e];
+            if (x < 64) {
+                const int b = bd >> 8;
+                float b1;
+                if (b1mode == 0) b1 = (x == b) ? 1.f : 0.f;
+                else if (b1mode == 1) b1 = FT[x * kLd + b];
+                else b1 = B1g[b * 64 + x];
+                U[e * 64 + x] = ent_v[e0 + e] * b1;
+            } else {
+                W[e * 64 + x - 64] = FT[(x - 64) * kLd + (bd & 255)];
+            }
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int e = 0; e < ne; ++e) {
+            const float4 wv = *reinterpret_cast<const float4*>(W + e * 64 + io.col0());
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = reinterpret_cast<const float4*>(tab)[threadIdx.x + 256 * i];
+            for (int i = 0; i < 4; ++i) {
+                const float u = U[e * 64 + io.row(i)];
+                r[i][0] = fmaf(-u, wv.x, r[i][0]);
+                r[i][1] = fmaf(-u, wv.y, r[i][1]);
+                r[i][2] = fmaf(-u, wv.z, r[i][2]);
+                r[i][3] = fmaf(-u, wv.w, r[i][3]);
+            }
+        }
     }
-    // ... and land (LDS), later, so the loads fly under other work.
-    __device__ __forceinline__ void land(float* lds) const {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) reinterpret_cast<float4*>(lds)[threadIdx.x + 256 * i] = v[i];
-    }
-};
+}
 
 __device__ __forceinline__ int b1_mode(const ga_demo_tensor& td) {
     return td.n1 == 1 ? 0 : (td.basis1 == td.basis2 ? 1 : 2);
 }
 
-// Bitonic compare-exchange stage over 64*R values held as v[r] = element
-// r*64 + lane of a sequence being sorted ascending (`size`, `stride` as in
-// the textbook network; element e sorts ascending iff (e & size) == 0).
-template <int R>
-__device__ __forceinline__ void bitonic_stage(uint32_t (&v)[R], int e_base, int size, int stride) {
-    const int lane = threadIdx.x & 63;
-    if (stride >= 64) {
-        const int rs = stride >> 6;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int r2 = r ^ rs;
-            if (r2 > r) {
-                const bool asc = (((e_base + r * 64) & size) == 0);
-                const uint32_t a = v[r], b = v[r2];
-                v[r] = asc ? (a < b ? a : b) : (a > b ? a : b);
-                v[r2] = asc ? (a > b ? a : b) : (a < b ? a : b);
-            }
-        }
-    } else {
-        const bool lower = (lane & stride) == 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t o = __shfl_xor(v[r], stride, 64);
-            const bool asc = (((e_base + r * 64 + lane) & size) == 0);
-            v[r] = (lower == asc) ? (v[r] < o ? v[r] : o) : (v[r] > o ? v[r] : o);
-        }
-    }
-}
-
 // Selection bits (T-map: lane t owns coefficients 16t .. 16t+15 of the padded
 // row-major grid) of the k largest keys; ties at the k-th key -> lowest index.
-// Fast path (k <= 64): T0 = the k-th largest of the 256 per-lane maxima — a
-// lower bound on the k-th largest key, since >= k lanes hold a key >= T0 — by
-// a bitonic sort (each wave sorts its 64 maxima in registers, wave 0 merges
-// the four runs); the answer lies among the keys >= T0 (about k of them on
-// DCT coefficients), which are ranked exactly in LDS.  Falls back to a
-// 4-round 8-bit radix select when k > 64 or the candidates overflow (e.g. an
-// all-zero chunk, where every key ties).
+// Fast path (k <= 256): T0 = the k-th largest of the 256 per-lane maxima is a
+// lower bound on the k-th largest key (>= k lanes hold a key >= T0), found by
+// every wave redundantly with a 31-step bitwise search over the maxima
+// (ballot + popcount per step, no LDS traffic, no barrier).  The keys >= T0
+// (about k of them on DCT coefficients) are appended to an LDS list and ranked
+// exactly (key, then coefficient position).  Falls back to a 4-round 8-bit
+// radix select if the candidates overflow (e.g. an all-zero chunk, where every
+// key ties) or k > 256.
 __device__ uint32_t select_topk(const uint32_t (&key)[16], int k, uint32_t* tmax, uint32_t* cand_key,
                                 uint8_t* cand_sel, int* hist, int* misc) {
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int t = threadIdx.x, lane = t & 63;
+    constexpr int kCap = kCandMax / 2;                       // candidates: key[kCap], 16-bit position[kCap]
+    uint16_t* cpos = reinterpret_cast<uint16_t*>(cand_sel);  // cand_sel is kCandMax bytes
+    uint32_t* selw = tmax;                                   // selection words, reusing the maxima slots
     uint32_t mymax = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) mymax = key[j] > mymax ? key[j] : mymax;
-    bool fast = k <= 64;
-    uint32_t sel = 0;
-    if (fast) {
-        // sizes 2..64: every wave sorts its maxima (run w ascending iff w even)
-        uint32_t v1[1] = {mymax};
-        for (int size = 2; size <= 64; size <<= 1)
-            for (int stride = size >> 1; stride > 0; stride >>= 1) bitonic_stage<1>(v1, wid * 64, size, stride);
-        tmax[t] = v1[0];
+    if (k <= kDmBlock) {
+        if (t == 0) misc[3] = 0;  // candidate counter
+        tmax[t] = mymax;
         __syncthreads();
-        if (wid == 0) {  // sizes 128, 256: merge the four runs
-            uint32_t v4[4];
+        GA_STAMP(8);
+        uint32_t v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v4[r] = tmax[r * 64 + lane];
-            for (int size = 128; size <= 256; size <<= 1)
-                for (int stride = size >> 1; stride > 0; stride >>= 1) bitonic_stage<4>(v4, 0, size, stride);
-            const int e = 256 - k;
+        for (int r = 0; r < 4; ++r) v[r] = tmax[r * 64 + lane];
+        // bitwise search over the top 12 key bits (the exponent and 4 mantissa bits):
+        // any threshold <= the exact k-th largest maximum keeps the >= k guarantee
+        uint32_t T0 = 0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (r == (e >> 6) && lane == (e & 63)) misc[1] = (int)v4[r];
+        for (int bit = 30; bit >= 19; --bit) {
+            const uint32_t cand = T0 | (1u << bit);
+            int cnt = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cnt += __popcll(__ballot(v[r] >= cand));
+            if (cnt >= k) T0 = cand;
+        }
+        if (T0 == 0u) T0 = 1u;  // key 0 marks padding; small chunks rank all their keys
+        GA_STAMP(9);
+        __syncthreads();        // every wave has read the maxima: tmax becomes selw
+        selw[t] = 0u;
+        // append the candidates: per-wave ballot compaction, one LDS atomic per wave
+        uint64_t m[16];
+        int wcount = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            m[j] = __ballot(key[j] >= T0);
+            wcount += __popcll(m[j]);
+        }
+        int wbase = 0;
+        if (lane == 0 && wcount) wbase = atomicAdd(&misc[3], wcount);
+        wbase = __shfl(wbase, 0, 64);
+        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if ((m[j] >> lane) & 1ull) {
+                const int at = wbase + __popcll(m[j] & below);
+                if (at < kCap) {
+                    cand_key[at] = key[j];
+                    cpos[at] = (uint16_t)(16 * t + j);
+                }
+            }
+            wbase += __popcll(m[j]);
         }
         __syncthreads();
-        uint32_t T0 = (uint32_t)misc[1];
-        if (T0 == 0u) T0 = 1u;  // key 0 marks padding; small chunks rank all their keys
-        int cc = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) cc += key[j] >= T0;
-        int C;
-        const int cbase = scan256(cc, misc + 4, &C);
-        fast = C <= kCandMax;
-        if (fast) {
-            int w = cbase;
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (key[j] >= T0) cand_key[w++] = key[j];
-            __syncthreads();
+        const int C = misc[3];
+        GA_STAMP(10);
+#ifdef GA_DEMO_STAMPS
+        if (threadIdx.x == 0) g_demo_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + 12] = C;
+#endif
+        if (C <= kCap) {
             for (int i = t; i < C; i += kDmBlock) {
                 const uint32_t ki = cand_key[i];
+                const int pi = cpos[i];
                 int rank = 0;
                 for (int j = 0; j < C; ++j) {
                     const uint32_t kj = cand_key[j];
-                    rank += (kj > ki) | ((kj == ki) & (j < i));
+                    rank += (kj > ki) | ((kj == ki) & (cpos[j] < pi));
                 }
-                cand_sel[i] = rank < k;
+                if (rank < k) atomicOr(&selw[pi >> 4], 1u << (pi & 15));
             }
             __syncthreads();
-            w = cbase;
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (key[j] >= T0) sel |= (uint32_t)cand_sel[w++] << j;
-            return sel;
+            GA_STAMP(11);
+            return selw[t];
         }
+        __syncthreads();  // overflow: fall back to the radix select below
     }
+    uint32_t sel = 0;
     // radix select of the k-th largest key
     uint32_t prefix = 0, pmask = 0;
     int kk = k;
@@ -379,8 +380,8 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ F,
     const float* __restrict__ B, T* param, const T* __restrict__ grad, T* delta, int64_t ld, float lr,
     float decay, float wd_factor, int32_t* payload, int64_t pstride, int64_t M, int ptr_vec) {
-    __shared__ __attribute__((aligned(16))) float X[kTile];  // delta chunk (MFMA A operand); then the B2 table
-    __shared__ float Y[kTile];   // T = X.F2, Y = F1^T.T
+    __shared__ __attribute__((aligned(16))) float X[kTile];  // delta -> T -> Y (in place); then residual staging
+    __shared__ float FT[kTile];                               // basis F (row stride kLd)
     __shared__ uint32_t tmax[kDmBlock];
     __shared__ uint32_t cand_key[kCandMax];  // candidates; then the entry list
     __shared__ uint8_t cand_sel[kCandMax];
@@ -399,6 +400,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
     const ChunkIO io = chunk_io<T>(td, c, ld, ptr_vec != 0);
     const int n1 = td.n1, n2 = td.n2, k = td.k;
     GA_STAMP(0);
+    stage_basis<false>(FT, F + (int64_t)td.basis2 * 4096);
 
     // 1. error feedback in registers: x = decay*delta + lr*grad (+ decoupled weight decay on p)
     float x[4][4];
@@ -427,18 +429,19 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
     __syncthreads();
     GA_STAMP(1);
 
-    // 2. Y = F1^T . X . F2 on the matrix cores
-    f32x16 acc = mm64<true, false>(X, F + (int64_t)td.basis2 * 4096);
-    store_acc(Y, acc);
+    // 2. Y = F1^T . X . F2 on the matrix cores, in place in X
+    f32x16 acc = mm64<TILE_ROW, TILE_ROW>(X, FT);  // T = X . F2
+    __syncthreads();
+    store_acc(X, acc);
     __syncthreads();
     GA_STAMP(2);
-    TableStage bt;
-    bt.issue(B + (int64_t)td.basis2 * 4096);  // lands in X (free now) after the product
-    acc = mm64<false, true>(F + (int64_t)td.basis1 * 4096, Y);
-    __syncthreads();
-    store_acc(Y, acc);
-    bt.land(X);
-    __syncthreads();
+    if (n1 > 1) {
+        if (td.basis1 == td.basis2) acc = mm64<TILE_COL, TILE_ROW>(FT, X);  // F1^T . T
+        else acc = mm64<GTAB_COL, TILE_ROW>(F + (int64_t)td.basis1 * 4096, X);
+        __syncthreads();
+        store_acc(X, acc);
+        __syncthreads();
+    }  // n1 == 1: F1 = [1], Y = T
     GA_STAMP(3);
 
     // 3. top-k of |Y| over the valid n1 x n2 coefficients
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const bool valid = row < n1 && (col0 + j) < n2;
-        key[j] = valid ? (__float_as_uint(Y[row * kLd + col0 + j]) & 0x7fffffffu) + 1u : 0u;
+        key[j] = valid ? (__float_as_uint(X[row * kLd + col0 + j]) & 0x7fffffffu) + 1u : 0u;
     }
     const uint32_t sel = select_topk(key, k, tmax, cand_key, cand_sel, hist, misc);
     GA_STAMP(4);
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         if (sel & (1u << j)) {
-            const float y = Y[row * kLd + col0 + j];
+            const float y = X[row * kLd + col0 + j];
             out_idx[slot] = row * n2 + col0 + j;
             out_val[slot] = y;
             ent_bd[slot] = (row << 8) | (col0 + j);
@@ -469,36 +472,25 @@ __global__ __launch_bounds__(kDmBlock) void demo_encode_kernel(
             ++slot;
         }
     }
-    __syncthreads();
     GA_STAMP(5);
 
     // 5. residual: delta = x - sum_e v_e * outer(B1[b_e, :], B2[d_e, :])  (the sparse
     //    form of B1^T . S . B2: k rank-1 terms instead of two dense products)
-    float r[4][4];
+    sparse_rank_update(x, ent_bd, ent_v, k, FT, B + (int64_t)td.basis1 * 4096, b1_mode(td), io, X);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) r[i][e] = 0.f;
-    sparse_rank_update(r, ent_bd, ent_v, k, X, B + (int64_t)td.basis1 * 4096, b1_mode(td), io, Y);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (io.live(i)) {
-            float o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = x[i][e] - r[i][e];
-            store4(delta, io, i, o);
-        }
-    }
+        if (io.live(i)) store4(delta, io, i, x[i]);
     GA_STAMP(6);
 }
 
-template <typename T>
+template <typename T, typename CntT>
 __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, const float* __restrict__ B,
     const int32_t* __restrict__ payload, int64_t pstride, int64_t M, int64_t nsrc, T* param, T* grad,
     int64_t K, int64_t ld, float lr, int ptr_vec) {
-    __shared__ float S[kTile];      // scatter-mean tile (row stride kLd), then the decoded g
-    __shared__ uint16_t cnt[4096];  // hits per coefficient
+    __shared__ float S[kTile];   // scatter-mean tile -> U -> g (in place)
+    __shared__ float FT[kTile];  // basis F (row stride kLd), staged from B = F^T
+    __shared__ CntT cnt[4096];   // hits per coefficient
     __shared__ int misc[4];
 
     const int chunk = blockIdx.x;
@@ -508,6 +500,7 @@ __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
     const int n2 = td.n2, nk = td.k, nvalid = td.n1 * td.n2;
     const ChunkIO io = chunk_io<T>(td, c, ld, ptr_vec != 0);
 
+    stage_basis<true>(FT, B + (int64_t)td.basis2 * 4096);
     for (int e = threadIdx.x; e < kTile; e += kDmBlock) S[e] = 0.f;
     for (int e = threadIdx.x; e < 4096; e += kDmBlock) cnt[e] = 0;
     __syncthreads();
@@ -537,15 +530,18 @@ __global__ __launch_bounds__(kDmBlock) void demo_decode_kernel(
         __syncthreads();
     }
 
-    // g = B1^T . S . B2 on the matrix cores, staged back through LDS for row-major I/O
-    f32x16 acc = mm64<true, false>(S, B + (int64_t)td.basis2 * 4096);
+    // g = B1^T . S . B2 = F1 . S . F2^T on the matrix cores, in place in S
+    f32x16 acc = mm64<TILE_ROW, TILE_COL>(S, FT);  // U = S . F2^T
     __syncthreads();
     store_acc(S, acc);
     __syncthreads();
-    acc = mm64<false, true>(B + (int64_t)td.basis1 * 4096, S);
-    __syncthreads();
-    store_acc(S, acc);
-    __syncthreads();
+    if (td.n1 > 1) {
+        if (td.basis1 == td.basis2) acc = mm64<TILE_ROW, TILE_ROW>(FT, S);  // F1 . U
+        else acc = mm64<GTAB_COL, TILE_ROW>(B + (int64_t)td.basis1 * 4096, S);  // F1[i][k] = B1[k][i]
+        __syncthreads();
+        store_acc(S, acc);
+        __syncthreads();
+    }
 
     // grad = sign(g) (torch.sign: NaN -> 0);  p -= lr * grad   (demo.py:200-209)
 #pragma unroll
@@ -623,19 +619,30 @@ extern "C" GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, i
     GA_REQUIRE(tensors && B && payload && param, "ga_demo_decode: null buffer");
     GA_REQUIRE(S >= 1 && K >= 1, "ga_demo_decode: bad S=%lld K=%lld", (long long)S, (long long)K);
     GA_REQUIRE(S == 1 || payload_stride >= 2 * M, "ga_demo_decode: payload_stride < 2*M");
+    GA_REQUIRE(S <= 65535, "ga_demo_decode: more than 65535 sources");
     GA_REQUIRE(K == 1 || ld > 0, "ga_demo_decode: bad ld");
     const int vb = dtype == GA_F32 ? 16 : 8;
     const int ptr_vec = ((uintptr_t)param % vb == 0) && (grad == nullptr || (uintptr_t)grad % vb == 0);
     switch (dtype) {
         case GA_F32:
-            hipLaunchKernelGGL((demo_decode_kernel<float>), dim3((unsigned)nchunks), dim3(kDmBlock), 0, stream,
-                               tensors, ntensors, B, payload, payload_stride, M, S, (float*)param, (float*)grad, K,
-                               ld, lr, ptr_vec);
+            if (S <= 255)
+                hipLaunchKernelGGL((demo_decode_kernel<float, uint8_t>), dim3((unsigned)nchunks), dim3(kDmBlock), 0,
+                                   stream, tensors, ntensors, B, payload, payload_stride, M, S, (float*)param,
+                                   (float*)grad, K, ld, lr, ptr_vec);
+            else
+                hipLaunchKernelGGL((demo_decode_kernel<float, uint16_t>), dim3((unsigned)nchunks), dim3(kDmBlock),
+                                   0, stream, tensors, ntensors, B, payload, payload_stride, M, S, (float*)param,
+                                   (float*)grad, K, ld, lr, ptr_vec);
             break;
         case GA_BF16:
-            hipLaunchKernelGGL((demo_decode_kernel<__hip_bfloat16>), dim3((unsigned)nchunks), dim3(kDmBlock), 0,
-                               stream, tensors, ntensors, B, payload, payload_stride, M, S, (__hip_bfloat16*)param,
-                               (__hip_bfloat16*)grad, K, ld, lr, ptr_vec);
+            if (S <= 255)
+                hipLaunchKernelGGL((demo_decode_kernel<__hip_bfloat16, uint8_t>), dim3((unsigned)nchunks),
+                                   dim3(kDmBlock), 0, stream, tensors, ntensors, B, payload, payload_stride, M, S,
+                                   (__hip_bfloat16*)param, (__hip_bfloat16*)grad, K, ld, lr, ptr_vec);
+            else
+                hipLaunchKernelGGL((demo_decode_kernel<__hip_bfloat16, uint16_t>), dim3((unsigned)nchunks),
+                                   dim3(kDmBlock), 0, stream, tensors, ntensors, B, payload, payload_stride, M, S,
+                                   (__hip_bfloat16*)param, (__hip_bfloat16*)grad, K, ld, lr, ptr_vec);
             break;
         default: set_error("ga_demo_decode: unknown dtype %d", dtype); return GA_EINVAL;
     }

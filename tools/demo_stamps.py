@@ -63,8 +63,14 @@ def main():
     print(f"workgroup lifetime cycles: median {np.median(tot):.0f}  p90 {np.percentile(tot, 90):.0f}")
     for i, name in enumerate(PHASES):
         print(f"  {name:22s} median {np.median(d[:, i]):8.0f} cyc  share {np.median(d[:, i]) / np.median(tot):6.1%}")
-    stg = stamps.view(-1, 16).cpu().numpy()[:, 7].astype(np.int64) - st[:, 5]
-    print(f"  (residual: staging of the first {32} entries median {np.median(stg):.0f} cyc)")
+    full = stamps.view(-1, 16).cpu().numpy().astype(np.int64)
+    topk_parts = [("keys+maxima->LDS", full[:, 8] - full[:, 3]), ("bitwise search", full[:, 9] - full[:, 8]),
+                  ("append candidates", full[:, 10] - full[:, 9]), ("rank candidates", full[:, 11] - full[:, 10]),
+                  ("return", full[:, 4] - full[:, 11])]
+    for name, v in topk_parts:
+        print(f"    top-k {name:18s} median {np.median(v):8.0f} cyc")
+    C = full[:, 12]
+    print(f"    candidates per chunk: median {np.median(C):.0f}  p90 {np.percentile(C, 90):.0f}  max {C.max()}")
 
 
 if __name__ == "__main__":
