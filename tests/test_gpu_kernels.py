@@ -419,3 +419,91 @@ def test_demo_all_zero_chunk_tie_rule():
     idx, val = _payload_host(payload, plan)
     assert (val == 0).all()
     assert all(np.array_equal(idx[0, c * 32:(c + 1) * 32], np.arange(32)) for c in range(4))
+
+
+@pytest.mark.parametrize("topk,chunk", [(300, 64), (8, 16), (64, 32)])
+def test_demo_topk_and_chunk_variants(topk, chunk):
+    """k > 256 (radix-select path), small chunks, k == chunk."""
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    shapes = [(128, 128), (96,), (32, 48)]
+    L = ArenaLayout(shapes)
+    plan = DemoPlan(L, chunk=chunk, topk=topk)
+    rng = np.random.default_rng(topk + chunk)
+    D = np.zeros((1, L.n), np.float32)
+    for o, nel in zip(L.offsets, L.numels):
+        D[0, o:o + nel] = rng.standard_normal(nel)
+    P, G, Dt = t(np.zeros_like(D)), t(np.zeros_like(D)), t(D)
+    payload = torch.zeros(1, 2 * plan.M, dtype=torch.int32, device=DEV)
+    ops.demo_encode(plan, P, G, Dt, payload, 0.01, 1.0 - 1e-9, 1.0)
+    gidx, gval = _payload_host(payload, plan)
+    e0 = 0
+    for ti, (shape, off, nel) in enumerate(zip(L.shapes, L.offsets, L.numels)):
+        R, C, n1, n2 = odemo.tensor_view(shape, chunk)
+        kk = max(1, min(topk, n1 * n2))
+        Y = odemo.encode(D[0, off:off + nel].reshape(shape), shape, chunk)
+        oidx, oval = odemo.topk_chunks(Y, topk)
+        margin = odemo.kth_margin(Y, topk).reshape(R // n1, C // n2)
+        ne = plan.entries_per_tensor[ti]
+        gi = gidx[0, e0:e0 + ne].reshape(R // n1, C // n2, kk)
+        for y in range(R // n1):
+            for x in range(C // n2):
+                if margin[y, x] > 1e-5:
+                    assert np.array_equal(gi[y, x], oidx[y, x]), (shape, y, x)
+        e0 += ne
+
+
+def test_demo_bf16_matches_oracle():
+    from gym_amd import ops
+    shapes = [(128, 128), (768,), (66, 128)]
+    L, plan, a = _demo_setup(shapes, 2, seed=11)
+    lr = 0.01
+    P = t(a["p"], torch.bfloat16)
+    G = t(a["g"], torch.bfloat16)
+    D = t(a["d"], torch.bfloat16)
+    p0 = P.float().cpu().numpy()
+    d0 = D.float().cpu().numpy()
+    g0 = G.float().cpu().numpy()
+    payload = torch.zeros(2, 2 * plan.M, dtype=torch.int32, device=DEV)
+    ops.demo_encode(plan, P, G, D, payload, lr, 0.999, 1.0)
+    Gs = torch.zeros_like(G)
+    ops.demo_decode(plan, payload, P, Gs, lr)
+    gP, gD = host(P), host(D)
+    for shape, off, nel in zip(L.shapes, L.offsets, L.numels):
+        want_p, want_d, want_s, _ = odemo.demo_step(p0[0, off:off + nel].reshape(shape),
+                                                    [d0[k, off:off + nel].reshape(shape) for k in range(2)],
+                                                    [g0[k, off:off + nel].reshape(shape) for k in range(2)], lr)
+        s = host(Gs)[0, off:off + nel].reshape(shape)
+        assert (s == want_s).mean() > 0.97
+        np.testing.assert_allclose(gP[0, off:off + nel].reshape(shape)[s == want_s], want_p[s == want_s],
+                                   rtol=1e-2, atol=1e-3)
+        for k in range(2):
+            np.testing.assert_allclose(gD[k, off:off + nel].reshape(shape), want_d[k], rtol=0,
+                                       atol=1e-2 * np.abs(want_d[k]).max())
+
+
+def test_sparta_bf16_and_many_replicas():
+    from gym_amd import ops
+    n, p = 200_003, 0.02
+    for K, dtype in ((4, torch.bfloat16), (64, torch.float32)):
+        x = np.random.default_rng(K).standard_normal((K, n)).astype(np.float32)
+        src = t(x, dtype)
+        xs = src.float().cpu().numpy()
+        m = osparta.philox_mask(n, 5, 6, p)
+        ops.sparta_average_local(src, n, float(K), seed=5, iteration=6, p=p)
+        want = osparta.sparse_average(list(xs), m)
+        got = host(src)
+        tol = 1e-2 if dtype == torch.bfloat16 else 0
+        for k in range(K):
+            np.testing.assert_allclose(got[k], want[k], rtol=tol, atol=tol)
+
+
+def test_replica_mean_edge_sizes():
+    from gym_amd import ops
+    empty = torch.zeros(0, device=DEV)
+    ops.replica_mean(empty.view(1, 0), empty.view(1, 0), n=0)
+    x = torch.arange(6, dtype=torch.float32, device=DEV).view(2, 3)  # ld 3: scalar path
+    out = torch.empty(3, device=DEV)
+    ops.replica_mean(x, out)
+    assert host(out).tolist() == [1.5, 2.5, 3.5]
