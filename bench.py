@@ -171,10 +171,10 @@ def bench_diloco(args, coll, dev):
     K_total = K * coll.world
     n_params = numel(shapes)
     value = K_total * 4 * n_params / t / 1e9
-    per = eng.per
+    per = int(np.mean(eng.launch_elems))  # elements per ga_diloco_outer launch (one per pipeline chunk)
     if coll.world == 1:  # read every replica, master, mom; write master, mom, every replica
         alg_bytes = (2 * K + 4) * per * 4
-    elif eng.shard:  # RCCL: read the reduce-scattered sum shard, master, mom; write master, mom, param shard
+    elif eng.shard:  # RCCL: read the reduce-scattered sum slice, master, mom; write master, mom, param slice
         alg_bytes = 6 * per * 4
     else:  # gloo rehearsal: read the all-reduced sum, master, mom; write master, mom, every replica
         alg_bytes = (5 + K) * per * 4

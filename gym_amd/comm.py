@@ -11,6 +11,16 @@ import torch
 import torch.distributed as dist
 
 
+class _Done:
+    """Handle of a collective that already completed (synchronous paths)."""
+
+    def wait(self):
+        return True
+
+
+DONE = _Done()
+
+
 class Collective:
     def __init__(self, group=None):
         self.group = group
@@ -26,46 +36,56 @@ class Collective:
         return self.backend == "nccl"
 
     # -- collectives (no-ops at world size 1) --------------------------------
-    def all_reduce_(self, t):
+    # With async_op=True the RCCL forms return the torch Work handle (its
+    # wait() orders the CURRENT stream after the collective, the host does not
+    # block); every other case runs synchronously and returns DONE.
+    def all_reduce_(self, t, async_op=False):
         if self.world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-        return t
+            w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op and self.rccl)
+            if async_op:
+                return w if w is not None else DONE
+        return DONE if async_op else t
 
     def broadcast_(self, t, src=0):
         if self.world > 1:
             dist.broadcast(t, src=src, group=self.group)
         return t
 
-    def reduce_scatter(self, shard_out, full):
+    def reduce_scatter(self, shard_out, full, async_op=False):
         """shard_out = rank's shard of sum over ranks of `full` (full is scratch:
         the gloo fallback reduces it in place)."""
         if self.world == 1:
             if shard_out.data_ptr() != full.data_ptr():
                 shard_out.copy_(full[: shard_out.numel()])
-            return shard_out
+            return DONE if async_op else shard_out
         if self.rccl:
-            dist.reduce_scatter_tensor(shard_out, full, op=dist.ReduceOp.SUM, group=self.group)
+            w = dist.reduce_scatter_tensor(shard_out, full, op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=async_op)
+            if async_op:
+                return w
         else:
             dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group)
             per = shard_out.numel()
             shard_out.copy_(full[self.rank * per:(self.rank + 1) * per])
-        return shard_out
+        return DONE if async_op else shard_out
 
-    def all_gather_into(self, full, shard):
+    def all_gather_into(self, full, shard, async_op=False):
         """full[r*per:(r+1)*per] = shard of rank r.  `shard` may be the rank's
         own slice of `full` (in place)."""
         if self.world == 1:
             if full.data_ptr() != shard.data_ptr():
                 full[: shard.numel()].copy_(shard)
-            return full
+            return DONE if async_op else full
         if self.rccl:
-            dist.all_gather_into_tensor(full, shard, group=self.group)
+            w = dist.all_gather_into_tensor(full, shard, group=self.group, async_op=async_op)
+            if async_op:
+                return w
         else:
             per = shard.numel()
             parts = list(full.split(per))
             src = shard.clone() if shard.data_ptr() == parts[self.rank].data_ptr() else shard
             dist.all_gather(parts, src, group=self.group)
-        return full
+        return DONE if async_op else full
 
 
 def world_and_rank(group=None):

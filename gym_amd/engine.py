@@ -26,19 +26,121 @@ def _f32(x):
     return float(np.float32(x))
 
 
-class MeanReduce:
-    """Every replica <- (sum over all K_total nodes) / K_total."""
+CHUNK_BYTES = 64 << 20  # pipeline chunk of the sharded exchange (RCCL stays at its large-message rate)
 
-    def __init__(self, coll: Collective, K_local, n, device, dtype):
+
+class ShardPlan:
+    """Chunked reduce-scatter / all-gather plan over a flat arena of n elements.
+
+    The arena is cut into C contiguous chunks (each a multiple of world*64
+    elements); rank r owns the r-th 1/world slice of every chunk.  Its shard
+    state (DiLoCo master/momentum, the reduce-scatter output) is the
+    concatenation of those slices in chunk order.  Chunking lets the local
+    kernels of chunk c+1 run while RCCL moves chunk c (software pipeline, see
+    run())."""
+
+    def __init__(self, n, world, rank, elem_bytes, chunks=None, align=64):
+        unit = world * align
+        if n % unit:
+            raise ValueError(f"arena length {n} is not a multiple of world*{align} = {unit}")
+        units = n // unit
+        if chunks is None:
+            chunks = max(1, -(-n * elem_bytes // CHUNK_BYTES))
+        C = max(1, min(int(chunks), units))
+        base, rem = divmod(units, C)
+        self.n, self.world, self.rank = n, world, rank
+        self.bounds, self.own, self.shard = [], [], []
+        c0 = m0 = 0
+        for i in range(C):
+            cs = (base + (1 if i < rem else 0)) * unit
+            pcs = cs // world
+            self.bounds.append((c0, c0 + cs))
+            self.own.append((c0 + rank * pcs, c0 + (rank + 1) * pcs))
+            self.shard.append((m0, m0 + pcs))
+            c0 += cs
+            m0 += pcs
+        self.per = m0
+
+    def gather_shard(self, flat, out):
+        """out <- this rank's slices of `flat` (shard layout)."""
+        for (a, b), (m0, m1) in zip(self.own, self.shard):
+            out[m0:m1].copy_(flat[a:b])
+
+    def run(self, coll, reps, rs_out, shard_fn):
+        """One exchange over replica set reps [K, >= n] (K >= 1):
+          per chunk c:  reps[0,c] <- sum_k reps[k,c]          (K > 1, in place)
+                        rs_out[shard c] <- reduce-scatter over ranks (RCCL)
+                        shard_fn(rs_out[shard c], (m0, m1), reps[0, own c])
+                        reps[0,c] <- all-gather of the owned slices (RCCL)
+                        reps[1:,c] <- reps[0,c]                (K > 1)
+        Issued with a lag of one chunk between the stages so the local
+        kernels (current stream) overlap the collectives (RCCL stream):
+        chunk c+1's sum runs while chunk c is reduce-scattered, chunk c-1's
+        replica write-back while chunk c is all-gathered.  Work.wait() only
+        orders the current stream after a collective; the host never blocks."""
+        K = reps.shape[0]
+        row0 = reps[0]
+        rs_q, ag_q = [], []
+
+        def finish_rs(i, w):
+            w.wait()
+            a, b = self.own[i]
+            m0, m1 = self.shard[i]
+            shard_fn(rs_out[m0:m1], (m0, m1), row0[a:b])
+            c0, c1 = self.bounds[i]
+            ag_q.append((i, coll.all_gather_into(row0[c0:c1], row0[a:b], async_op=True)))
+
+        def finish_ag(i, w):
+            w.wait()
+            if K > 1:
+                c0, c1 = self.bounds[i]
+                ops.replica_mean(reps[0:1, c0:c1], reps[1:, c0:c1], divisor=1.0)
+
+        for i, (c0, c1) in enumerate(self.bounds):
+            if K > 1:
+                ops.replica_mean(reps[:, c0:c1], reps[0:1, c0:c1], divisor=1.0)
+            m0, m1 = self.shard[i]
+            rs_q.append((i, coll.reduce_scatter(rs_out[m0:m1], row0[c0:c1], async_op=True)))
+            if len(rs_q) > 1:
+                finish_rs(*rs_q.pop(0))
+            if len(ag_q) > 1:
+                finish_ag(*ag_q.pop(0))
+        while rs_q:
+            finish_rs(*rs_q.pop(0))
+        while ag_q:
+            finish_ag(*ag_q.pop(0))
+
+
+class MeanReduce:
+    """Every replica <- (sum over all K_total nodes) / K_total.
+
+    RCCL, world > 1: chunked reduce-scatter -> true division of the own slice
+    -> all-gather (ShardPlan.run: the division touches 1/world of the arena
+    and overlaps the exchange of the next chunk; the same bytes on the wire as
+    one all-reduce).  gloo: all-reduce of the (locally pre-summed) arena."""
+
+    def __init__(self, coll: Collective, K_local, n, device, dtype, shard=None, chunks=None):
         self.coll, self.K_local, self.n = coll, int(K_local), int(n)
         self.K_total = coll.world * self.K_local
-        self.sum = torch.empty(n, device=device, dtype=dtype) if (coll.world > 1 and K_local > 1) else None
+        W = coll.world
+        self.shard = (coll.rccl and W > 1) if shard is None else (shard and W > 1)
+        if self.shard:
+            esz = torch.empty((), dtype=dtype).element_size()
+            self.plan = ShardPlan(self.n, W, coll.rank, esz, chunks)
+            self.rs_out = torch.empty(self.plan.per, device=device, dtype=dtype)
+        self.sum = torch.empty(n, device=device, dtype=dtype) if (W > 1 and K_local > 1 and not self.shard) else None
+
+    def _divide(self, rs_shard, m, own):
+        ops.replica_mean(rs_shard, own, divisor=self.K_total)
 
     def __call__(self, reps):
         K, n = self.K_local, self.n
         if self.coll.world == 1:
             if K > 1:
                 ops.replica_mean(reps, reps, n=n)
+            return
+        if self.shard:
+            self.plan.run(self.coll, reps[:, :n], self.rs_out, self._divide)
             return
         if K == 1:
             self.coll.all_reduce_(reps[0, :n])
@@ -51,12 +153,13 @@ class MeanReduce:
 
 class DiLoCoOuter:
     """Fused DiLoCo outer step.  With RCCL and world > 1 the master copy and
-    the momentum are sharded: reduce-scatter(sum) -> fused update of the own
-    shard -> all-gather(params); the same bytes on the wire as the reference's
-    all-reduce + broadcast, the outer-optimizer state / G per GPU."""
+    the momentum are sharded: chunked reduce-scatter(sum) -> fused update of
+    the own slice -> all-gather(params), software-pipelined over chunks
+    (ShardPlan.run); the same bytes on the wire as the reference's all-reduce
+    + broadcast, the outer-optimizer state / world per GPU."""
 
     def __init__(self, coll: Collective, K_local, n, device, dtype, lr=0.7, momentum=0.9, nesterov=True,
-                 dampening=0.0, weight_decay=0.0, shard=None):
+                 dampening=0.0, weight_decay=0.0, shard=None, chunks=None):
         self.coll, self.K_local = coll, int(K_local)
         self.K_total = coll.world * self.K_local
         self.hp = dict(lr=lr, momentum=momentum, nesterov=nesterov, dampening=dampening, weight_decay=weight_decay)
@@ -64,56 +167,52 @@ class DiLoCoOuter:
         self.shard = (coll.rccl and W > 1) if shard is None else (shard and W > 1)
         self.n = int(n)
         if self.shard:
-            assert n % W == 0, "arena must be padded to a multiple of the world size"
-            self.per = n // W
-            self.lo = coll.rank * self.per
-            self.hi = self.lo + self.per
+            esz = torch.empty((), dtype=dtype).element_size()
+            self.plan = ShardPlan(self.n, W, coll.rank, esz, chunks)
+            self.per = self.plan.per
         else:
-            self.per, self.lo, self.hi = n, 0, n
+            self.plan = None
+            self.per = self.n
         self.master = torch.zeros(self.per, device=device, dtype=torch.float32)
         self.mom = torch.zeros(self.per, device=device, dtype=torch.float32) if momentum != 0 else None
         self.first = True
         self.dtype = dtype
-        needs_sum = W > 1 and (self.K_local > 1 or not self.shard)
-        self.sum = torch.empty(n, device=device, dtype=dtype) if needs_sum else None
+        self.sum = torch.empty(n, device=device, dtype=dtype) if (W > 1 and not self.shard) else None
         self.rs_out = torch.empty(self.per, device=device, dtype=dtype) if self.shard else None
-        self.gather = torch.empty(n, device=device, dtype=dtype) if (self.shard and self.K_local > 1) else None
+        self.launch_elems = []  # elements per ga_diloco_outer launch of the last step (bench roofline)
 
     def init_master(self, params_flat):
         """master <- the node's initial parameters (diloco.py:81-82)."""
-        self.master.copy_(params_flat[self.lo:self.hi])
+        if self.shard:
+            self.plan.gather_shard(params_flat, self.master)
+        else:
+            self.master.copy_(params_flat[:self.per])
         self.first = True
 
-    def _outer(self, src, divisor, dst):
+    def _outer(self, src, divisor, dst, m0=0, m1=None):
         h = self.hp
-        ops.diloco_outer(src, self.master, self.mom, dst, self.per, divisor, h["lr"], h["momentum"], h["dampening"],
-                         h["weight_decay"], h["nesterov"], self.first)
-        self.first = False
+        m1 = self.per if m1 is None else m1
+        mom = self.mom[m0:m1] if self.mom is not None else None
+        ops.diloco_outer(src, self.master[m0:m1], mom, dst, m1 - m0, divisor, h["lr"], h["momentum"],
+                         h["dampening"], h["weight_decay"], h["nesterov"], self.first)
+        self.launch_elems.append(m1 - m0)
+
+    def _outer_shard(self, rs_shard, m, own):
+        self._outer(rs_shard, self.K_total, own, m[0], m[1])
 
     def __call__(self, reps):
-        n, K = self.n, self.K_local
+        n = self.n
         W = self.coll.world
+        self.launch_elems = []
         if W == 1:  # one kernel: read every replica, update, write every replica
             self._outer(reps[:, :n], self.K_total, reps[:, :n])
-            return
-        if not self.shard:  # gloo: all-reduce the sum, replicated update
+        elif not self.shard:  # gloo: all-reduce the sum, replicated update
             ops.replica_mean(reps, self.sum, n=n, divisor=1.0)
             self.coll.all_reduce_(self.sum)
             self._outer(self.sum, self.K_total, reps[:, :n])
-            return
-        src_full = reps[0, :n] if K == 1 else self.sum
-        if K > 1:
-            ops.replica_mean(reps, self.sum, n=n, divisor=1.0)
-        self.coll.reduce_scatter(self.rs_out, src_full)
-        if K == 1:
-            own = reps[0, self.lo:self.hi]
-            self._outer(self.rs_out, self.K_total, own)
-            self.coll.all_gather_into(reps[0, :n], own)
         else:
-            own = self.gather[self.lo:self.hi]
-            self._outer(self.rs_out, self.K_total, own)
-            self.coll.all_gather_into(self.gather, own)
-            ops.replica_mean(self.gather, reps, n=n, divisor=1.0)
+            self.plan.run(self.coll, reps[:, :n], self.rs_out, self._outer_shard)
+        self.first = False
 
 
 def sparta_capacity(n, p):

@@ -99,5 +99,26 @@ def check_demo(res, world, golden_dir):
                 np.testing.assert_allclose(res[r][f"delta_{step}_{i}"], ref_d, rtol=0, atol=2e-5 * scale)
 
 
-CHECKS = {"simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
+def check_engine(res, world, golden_dir, K_local=3):
+    """Every node of every rank ends equal to the oracle over all K_total nodes
+    (reordered fp32 sums: RCCL/gloo ring order, 1e-6 relative)."""
+    import strategy_scenarios as S
+    from oracle import diloco as odiloco
+    from oracle import reduce as oreduce
+    KT = world * K_local
+    n = world * 64 * 10
+    x = [S.engine_node(j, n) for j in range(KT)]
+    m1, b1, _ = odiloco.outer_step(S.engine_node(0, n), None, x)
+    x2 = [m1 + S.engine_node(j, n, salt=1) * np.float32(0.05) for j in range(KT)]
+    m2, _, _ = odiloco.outer_step(m1, b1, x2)
+    avg = oreduce.mean_reduce([S.engine_node(j, n, salt=2) for j in range(KT)])
+    for r in range(world):
+        for k in range(K_local):
+            np.testing.assert_allclose(res[r]["d1"][k], m1, rtol=1e-6, atol=2e-8)
+            np.testing.assert_allclose(res[r]["d2"][k], m2, rtol=1e-6, atol=2e-8)
+            np.testing.assert_allclose(res[r]["m_shard"][k], avg, rtol=1e-6, atol=2e-8)
+            np.testing.assert_allclose(res[r]["m_plain"][k], avg, rtol=1e-6, atol=2e-8)
+
+
+CHECKS = {"engine": check_engine, "simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
           "sparta_philox": check_sparta_philox, "fedavg": check_fedavg, "demo": check_demo}

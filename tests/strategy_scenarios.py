@@ -40,13 +40,17 @@ def _host(t):
 
 
 # ------------------------------------------------------------------ scenarios --
-def sc_simple(rank, world, dev, golden_dir):
+def sc_simple(rank, world, dev, golden_dir, shard=None, chunks=None):
     from gym_amd.strategy import OptimSpec, SimpleReduceStrategy
     z = np.load(os.path.join(golden_dir, "mean_reduce.npz"))
     shapes = [z[f"K{world}_in_{si}"].shape[1:] for si in range(4)]
     model = ShapeModel(shapes, seed=1).to(dev)
     s = SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.SGD, lr=0.0))
     s._init_node(model, rank, world)
+    if shard is not None:  # the chunked reduce-scatter / divide / all-gather path, on gloo too
+        from gym_amd.engine import MeanReduce
+        a = s.arena
+        s.engine = MeanReduce(s.coll, 1, a.n, a.device, a.dtype, shard=shard, chunks=chunks)
     s.zero_grad()
     for si, p in enumerate(model.parameters()):
         p.grad = torch.from_numpy(z[f"K{world}_in_{si}"][rank]).to(dev)  # not the arena view: sync_grads copies
@@ -54,7 +58,7 @@ def sc_simple(rank, world, dev, golden_dir):
     return {f"grad_{si}": _host(p.grad) for si, p in enumerate(model.parameters())}
 
 
-def sc_diloco(rank, world, dev, golden_dir, shard=None):
+def sc_diloco(rank, world, dev, golden_dir, shard=None, chunks=None):
     from gym_amd.strategy import DiLoCoStrategy, OptimSpec
     z = np.load(os.path.join(golden_dir, "diloco.npz"))
     ns, calls, H = int(z["nshapes"]), int(z["calls"]), int(z["H"])
@@ -65,7 +69,7 @@ def sc_diloco(rank, world, dev, golden_dir, shard=None):
     if shard is not None:  # exercise the sharded (reduce-scatter/all-gather) path on gloo too
         from gym_amd.engine import DiLoCoOuter
         a = s.arena
-        s.engine = DiLoCoOuter(s.coll, 1, a.n, a.device, a.dtype, shard=shard)
+        s.engine = DiLoCoOuter(s.coll, 1, a.n, a.device, a.dtype, shard=shard, chunks=chunks)
         s.engine.init_master(a.flat)
     out = {}
     for call in range(calls):
@@ -184,7 +188,37 @@ def sc_demo(rank, world, dev, golden_dir):
     return out
 
 
-SCENARIOS = {"simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
+def engine_node(j, n, salt=0):
+    """Node j's synthetic arena for the batched-replica engine scenario."""
+    g = np.random.default_rng(100 + 1000 * salt + j)
+    return (g.standard_normal(n) * 0.02).astype(np.float32)
+
+
+def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4):
+    """Batched replicas on every rank (K_local nodes per process) through the
+    sharded, chunk-pipelined exchange: DiLoCo outer steps and the mean reduce."""
+    from gym_amd.comm import Collective
+    from gym_amd.engine import DiLoCoOuter, MeanReduce
+    coll = Collective()
+    n = world * 64 * 10
+    nodes = range(rank * K_local, (rank + 1) * K_local)
+    reps = torch.from_numpy(np.stack([engine_node(j, n) for j in nodes])).to(dev)
+    out = {}
+    eng = DiLoCoOuter(coll, K_local, n, dev, torch.float32, shard=True, chunks=chunks)
+    eng.init_master(torch.from_numpy(engine_node(0, n)).to(dev))
+    eng(reps)
+    out["d1"] = _host(reps)
+    reps += torch.from_numpy(np.stack([engine_node(j, n, salt=1) for j in nodes]) * np.float32(0.05)).to(dev)
+    eng(reps)
+    out["d2"] = _host(reps)
+    for tag, shard in (("m_shard", True), ("m_plain", False)):
+        r2 = torch.from_numpy(np.stack([engine_node(j, n, salt=2) for j in nodes])).to(dev)
+        MeanReduce(coll, K_local, n, dev, torch.float32, shard=shard, chunks=3)(r2)
+        out[tag] = _host(r2)
+    return out
+
+
+SCENARIOS = {"engine": sc_engine, "simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
              "fedavg": sc_fedavg, "demo": sc_demo}
 
 

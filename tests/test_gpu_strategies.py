@@ -13,8 +13,9 @@ from scenario_checks import CHECKS
 pytestmark = pytest.mark.gpu
 
 CASES = [
-    ("simple", 2, {}), ("simple", 3, {}),
-    ("diloco", 3, {}), ("diloco", 3, {"shard": True}),
+    ("simple", 2, {}), ("simple", 3, {}), ("simple", 3, {"shard": True, "chunks": 3}),
+    ("diloco", 3, {}), ("diloco", 3, {"shard": True}), ("diloco", 3, {"shard": True, "chunks": 5}),
+    ("engine", 3, {}),
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": True}),
     ("sparta_philox", 2, {}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),

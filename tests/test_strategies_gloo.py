@@ -10,8 +10,9 @@ from conftest import GOLDEN
 from scenario_checks import CHECKS
 
 CASES = [
-    ("simple", 2, {}), ("simple", 3, {}),
-    ("diloco", 3, {}), ("diloco", 3, {"shard": True}),
+    ("simple", 2, {}), ("simple", 3, {}), ("simple", 3, {"shard": True, "chunks": 3}),
+    ("diloco", 3, {}), ("diloco", 3, {"shard": True}), ("diloco", 3, {"shard": True, "chunks": 5}),
+    ("engine", 3, {}), ("engine", 2, {"chunks": 1}),
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": False}),
     ("sparta_philox", 2, {}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),
