@@ -9,7 +9,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libgym_amd.so")
+# GYM_AMD_LIB: an alternative in-tree build of the same library (kernel variants
+# compared by tools/; the ABI must match this file)
+LIB_PATH = os.environ.get("GYM_AMD_LIB") or os.path.join(_HERE, "_lib", "libgym_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gym_amd.h")
 
 GA_F32 = 0

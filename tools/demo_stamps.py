@@ -19,7 +19,8 @@ from gym_amd.arena import ArenaLayout  # noqa: E402
 from gym_amd.demo_codec import DemoPlan  # noqa: E402
 from gym_amd.shapes import MODELS  # noqa: E402
 
-PHASES = ["load+error-feedback", "DCT product 1", "DCT product 2", "top-k select", "emit entries", "residual+store"]
+PHASES = ["error-feedback+prefetch", "DCT product 1", "DCT product 2", "top-k select+emit", "residual (MFMA)",
+          "delta store"]
 
 
 def main():
@@ -56,21 +57,16 @@ def main():
     run()
     e1.record()
     torch.cuda.synchronize()
-    st = stamps.view(-1, 16).cpu().numpy()[:, :7].astype(np.int64)
-    d = np.diff(st, axis=1)
-    tot = st[:, 6] - st[:, 0]
-    print(f"{model}: {plan.nchunks} chunks, kernel {e0.elapsed_time(e1):.3f} ms (stamped build)")
-    print(f"workgroup lifetime cycles: median {np.median(tot):.0f}  p90 {np.percentile(tot, 90):.0f}")
+    st = stamps.view(-1, 16).cpu().numpy().astype(np.int64)
+    st = st[st[:, 8] > 0]  # workgroups that ran (persistent grid)
+    tot = st[:, :6].sum(axis=1)
+    nch = st[:, 8]
+    print(f"{model}: {plan.nchunks} chunks over {len(st)} workgroups, kernel {e0.elapsed_time(e1):.3f} ms "
+          f"(stamped build)")
+    print(f"cycles per chunk (workgroup view): median {np.median(tot / nch):.0f}")
     for i, name in enumerate(PHASES):
-        print(f"  {name:22s} median {np.median(d[:, i]):8.0f} cyc  share {np.median(d[:, i]) / np.median(tot):6.1%}")
-    full = stamps.view(-1, 16).cpu().numpy().astype(np.int64)
-    topk_parts = [("keys+maxima->LDS", full[:, 8] - full[:, 3]), ("bitwise search", full[:, 9] - full[:, 8]),
-                  ("append candidates", full[:, 10] - full[:, 9]), ("rank candidates", full[:, 11] - full[:, 10]),
-                  ("return", full[:, 4] - full[:, 11])]
-    for name, v in topk_parts:
-        print(f"    top-k {name:18s} median {np.median(v):8.0f} cyc")
-    C = full[:, 12]
-    print(f"    candidates per chunk: median {np.median(C):.0f}  p90 {np.percentile(C, 90):.0f}  max {C.max()}")
+        v = st[:, i] / nch
+        print(f"  {name:22s} median {np.median(v):8.0f} cyc/chunk  share {np.median(st[:, i] / tot):6.1%}")
 
 
 if __name__ == "__main__":

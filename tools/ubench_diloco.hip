@@ -106,6 +106,44 @@ __global__ __launch_bounds__(256) void v_static(const float* src, long ld, long 
     }
 }
 
+// the library's mapping: workgroup b owns vectors [b*CH, (b+1)*CH); U vectors per lane in flight
+template <int K, int CH, int U, bool NTS>
+__global__ __launch_bounds__(256) void v_chunk(const float* src, long ld, long n, float* master, float* mom, OP op,
+                                               float* dst) {
+    const long nv = n >> 2;
+    const long lo = (long)blockIdx.x * CH;
+    const long hi = lo + CH < nv ? lo + CH : nv;
+    for (long v0 = lo + threadIdx.x; v0 < hi; v0 += 256 * U) {
+        float4 x[U][K], m[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long v = v0 + 256L * u;
+            if (v < hi) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) x[u][k] = reinterpret_cast<const float4*>(src + k * ld)[v];
+                m[u] = reinterpret_cast<const float4*>(master)[v];
+                b[u] = reinterpret_cast<const float4*>(mom)[v];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long v = v0 + 256L * u;
+            if (v < hi) {
+                float a[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < K; ++k) { a[0] += x[u][k].x; a[1] += x[u][k].y; a[2] += x[u][k].z; a[3] += x[u][k].w; }
+                float4 o;
+                o.x = upd(a[0], m[u].x, b[u].x, op); o.y = upd(a[1], m[u].y, b[u].y, op);
+                o.z = upd(a[2], m[u].z, b[u].z, op); o.w = upd(a[3], m[u].w, b[u].w, op);
+                st4<NTS>(reinterpret_cast<float4*>(master) + v, m[u]);
+                st4<NTS>(reinterpret_cast<float4*>(mom) + v, b[u]);
+#pragma unroll
+                for (int k = 0; k < K; ++k) st4<NTS>(reinterpret_cast<float4*>(dst + k * ld) + v, o);
+            }
+        }
+    }
+}
+
 __global__ void copy4(const float4* a, float4* b, long nv) {
     long stride = (long)gridDim.x * blockDim.x;
     for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) b[v] = a[v];
@@ -158,6 +196,22 @@ int main() {
         float ms = time_ms([&] { v_static<K, U, NTL, NTS><<<g, 256>>>(src, ld, n, master, mom, op, src); }, reps); \
         printf("static U=%d ntl=%d nts=%d grid %5d: %.3f ms  %.0f GB/s\n", U, NTL, NTS, g, ms, bytes / ms / 1e6); \
     }
+#define RUNC(CH, U, NTS)                                                                                   \
+    {                                                                                                     \
+        int g = (int)((n / 4 + CH - 1) / CH);                                                             \
+        float ms = time_ms([&] { v_chunk<K, CH, U, NTS><<<g, 256>>>(src, ld, n, master, mom, op, src); }, reps); \
+        printf("chunk CH=%d U=%d nts=%d grid %6d: %.3f ms  %.0f GB/s\n", CH, U, NTS, g, ms, bytes / ms / 1e6); \
+    }
+    RUNC(1024, 1, false)
+    RUNC(1024, 1, false)
+    RUNC(512, 1, false)
+    RUNC(2048, 1, false)
+    RUNC(4096, 1, false)
+    RUNC(1024, 2, false)
+    RUNC(2048, 2, false)
+    RUNC(1024, 1, true)
+    RUNC(2048, 2, true)
+    if (getenv("ONLY_CHUNK")) return 0;
     RUN(1, false, false)
     RUN(2, false, false)
     RUN(1, false, true)
