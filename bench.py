@@ -18,7 +18,8 @@ cpu_baseline = the numpy oracle's outer step (oracle/diloco.py) on rank 0, on a
 
 Extra lines in "extras" (same timing rules, not the headline): SPARTA (K=32
 replicas per GPU, p=0.005, Philox mask), SimpleReduce (char-level nanoGPT,
-8 replicas per GPU), DeMo (GPT-2 350M, one node per GPU, chunk 64 / top-k 32).
+8 replicas per GPU), DeMo (GPT-2 350M, one node per GPU, chunk 64 / top-k 32),
+the inner AdamW + clip step on one GPT-2 124M arena (fused vs torch foreach).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-extras]
        torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -265,6 +266,42 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
             "ref_bytes_tx": plan.reference_bytes()}
 
 
+def bench_inner_adamw(args, coll, dev, model="gpt2-124m", max_norm=1.0):
+    """Inner optimizer step on one node's arena: fused
+    clip + AdamW (ga_grad_clip_coef + ga_adam_step) vs torch.optim.AdamW
+    (foreach, the reference's default) + clip_grad_norm_ on the same GPU."""
+    from gym_amd.arena import ParamArena
+    from gym_amd.fused_optim import ArenaAdam
+    shapes = MODELS[model]()
+    params = [torch.nn.Parameter(torch.randn(*sh, device=dev) * 0.02) for sh in shapes]
+    arena = ParamArena(params)
+    arena.grad_flat.normal_(0.0, 1e-3)
+    opt = ArenaAdam(params, arena, lr=1e-3)
+    timer = KernelTimer()
+    ops_adam = ops.adam_step
+    ops.adam_step = timer.wrap(ops.adam_step)
+    timer.on = True
+    t = timed_loop(lambda: opt.step(max_norm=max_norm), args.steps, args.warmup, coll)
+    kern = timer.mean_ms()
+    ops.adam_step = ops_adam
+    tparams = [torch.nn.Parameter(torch.randn(*sh, device=dev) * 0.02) for sh in shapes]
+    for p in tparams:
+        p.grad = torch.randn_like(p) * 1e-3
+    topt = torch.optim.AdamW(tparams, lr=1e-3, foreach=True)
+
+    def ref_step():
+        torch.nn.utils.clip_grad_norm_(tparams, max_norm)
+        topt.step()
+
+    tt = timed_loop(ref_step, args.steps, args.warmup, coll)
+    n = arena.n
+    alg = 28 * n  # read p, g, m, v; write p, m, v
+    return {"model": model, "n": n, "ms_per_step": round(t * 1e3, 4), "kernel_ms": round(kern, 4),
+            "kernel_GBps": round(alg / (kern * 1e-3) / 1e9, 1),
+            "kernel_frac_hbm": round(alg / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "torch_adamw_foreach_ms": round(tt * 1e3, 4), "speedup_vs_torch": round(tt / t, 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -274,7 +311,7 @@ def main():
     ap.add_argument("--replicas", type=int, default=8, help="simulated nodes per GPU")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--only", default=None, help="diloco|sparta|simple|demo (profiling runs)")
+    ap.add_argument("--only", default=None, help="diloco|sparta|simple|demo|adamw (profiling runs)")
     args = ap.parse_args()
 
     coll = setup_dist(args.gpus)
@@ -282,7 +319,8 @@ def main():
     torch.backends.cuda.matmul.allow_tf32 = False
 
     if args.only and args.only != "diloco":
-        fn = {"sparta": bench_sparta, "simple": bench_simple, "demo": bench_demo}[args.only]
+        fn = {"sparta": bench_sparta, "simple": bench_simple, "demo": bench_demo,
+              "adamw": bench_inner_adamw}[args.only]
         r = fn(args, coll, dev)
         if coll.rank == 0:
             print(json.dumps({"only": args.only, **r}), flush=True)
@@ -292,7 +330,7 @@ def main():
     extras = {}
     if not args.no_extras:
         for name, fn in (("sparta_k32", bench_sparta), ("simple_reduce_char_k8", bench_simple),
-                         ("demo_350m", bench_demo)):
+                         ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)):
             torch.cuda.empty_cache()
             try:
                 extras[name] = fn(args, coll, dev)

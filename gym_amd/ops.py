@@ -193,3 +193,32 @@ def demo_decode(plan, gathered, param, grad, lr):
     check(lib().ga_demo_decode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.B), _p(ga),
                                ga.stride(0), plan.M, S, _p(p2), _p(g2), K, ld, float(lr), _stream()),
           "ga_demo_decode")
+
+
+def sumsq_partials(device):
+    return torch.empty(int(lib().ga_sumsq_partials_count()), dtype=torch.float32, device=device)
+
+
+def grad_clip_coef(grad, n, max_norm, partials, out):
+    """out[0] <- min(1, max_norm / (||grad[:n]||_2 + 1e-6)), out[1] <- the norm (device side)."""
+    _gpu(grad, partials, out)
+    if partials.numel() < lib().ga_sumsq_partials_count() or out.numel() < 2 or out.dtype != torch.float32:
+        raise ValueError("grad_clip_coef: partials/out too small")
+    check(lib().ga_grad_clip_coef(_dtype_code(grad), _p(grad), int(n), float(max_norm), _p(partials), _p(out),
+                                  _stream()), "ga_grad_clip_coef")
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size,
+              bc2_sqrt, clip_coef=None):
+    """One fused Adam/AdamW step over fp32 flat buffers of equal length (see include/gym_amd.h)."""
+    _gpu(param, grad, exp_avg, exp_avg_sq, clip_coef)
+    n = param.numel()
+    for t in (grad, exp_avg, exp_avg_sq):
+        if t.numel() != n or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("adam_step: param/grad/exp_avg/exp_avg_sq must be contiguous fp32 of one length")
+    if param.dtype != torch.float32 or not param.is_contiguous():
+        raise TypeError("adam_step: fused path is fp32 only")
+    check(lib().ga_adam_step(_dtype_code(param), _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), n,
+                             float(lerp_w), float(beta2), float(one_m_beta2), float(eps), float(wd_factor),
+                             float(l2_wd), float(step_size), float(bc2_sqrt), _p(clip_coef), _stream()),
+          "ga_adam_step")

@@ -14,7 +14,7 @@ from typing import List, Optional, Union
 import torch
 
 from .optim import OptimSpec, ensure_optim_spec
-from .strategy import Strategy, clip_arena_grad_norm_
+from .strategy import Strategy, build_inner_optimizer, clip_and_step
 
 
 class CommunicationModule(ABC):
@@ -42,10 +42,7 @@ class CommunicateOptimizeStrategy(Strategy):
             m.strategy = self
 
     def step(self):
-        if self.max_norm:
-            self.arena.sync_grads()
-            clip_arena_grad_norm_(self.arena.grad_flat, self.max_norm)
-        self.optim.step()
+        clip_and_step(self, self.max_norm)
         self._communicate()
         super().step()
 
@@ -58,5 +55,5 @@ class CommunicateOptimizeStrategy(Strategy):
         self._bind_arena(model)
         for m in self.communication_modules:
             m._init_node(model, rank, num_nodes)
-        self.optim = self.inner_optim_spec.build(model)
+        self.optim = build_inner_optimizer(self.inner_optim_spec, model, self.arena)
         self._setup_scheduler()

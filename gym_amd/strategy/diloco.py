@@ -21,7 +21,7 @@ import torch
 from .. import ops
 from ..engine import DiLoCoOuter
 from .optim import OptimSpec, ensure_optim_spec
-from .strategy import Strategy, clip_arena_grad_norm_
+from .strategy import Strategy, build_inner_optimizer, clip_and_step
 
 
 def fused_sgd_hparams(spec: OptimSpec):
@@ -68,7 +68,7 @@ class DiLoCoStrategy(Strategy):
             self.master = torch.nn.Parameter(arena.flat.detach().float().clone())
             self.outer_optimizer = self.outer_optim_spec.build([self.master])
             self._avg = torch.empty_like(arena.flat)
-        self.optim = self.inner_optim_spec.build(model)
+        self.optim = build_inner_optimizer(self.inner_optim_spec, model, arena)
         self._setup_scheduler()
 
     def _outer_step(self):
@@ -86,10 +86,7 @@ class DiLoCoStrategy(Strategy):
             self.arena.flat.copy_(self.master)
 
     def step(self):
-        if "max_norm" in self.kwargs:
-            self.arena.sync_grads()
-            clip_arena_grad_norm_(self.arena.grad_flat, self.kwargs["max_norm"])
-        self.optim.step()
+        clip_and_step(self, self.kwargs.get("max_norm"))  # diloco.py:52-59
         if self.local_step % self.H == 0 and self.local_step > 0:
             self._outer_step()
         super().step()

@@ -9,7 +9,8 @@ zero_grad(), __config__()).  What changes underneath:
 - SimpleReduce's per-parameter `all_reduce(grad); grad.div_(K)` loop
   (strategy.py:130-133) becomes ONE RCCL all-reduce over the gradient arena
   plus ONE division kernel (ga_replica_mean);
-- gradient clipping runs over the arena (one norm, one scale);
+- gradient clipping + the default AdamW step run over the arena as one norm
+  reduction and one fused kernel (gym_amd.fused_optim.ArenaAdam);
 - zero_grad() zeroes the gradient arena in place (grads stay bound to it)
   instead of setting them to None.
 """
@@ -33,6 +34,32 @@ def require_gpu(device):
     if torch.device(device).type != "cuda":
         raise RuntimeError(f"gym_amd strategies run on MI355X GPUs; the model is on {device}. "
                            "Move it to a cuda device (one process per GPU).")
+
+
+def build_inner_optimizer(spec, model, arena):
+    """The node's inner optimizer: torch's AdamW/Adam become ArenaAdam (one fused
+    kernel over the arena per step, gym_amd.fused_optim); any other OptimSpec is
+    built as in the reference (OptimSpec.build, optim.py:38-39).  GA_FUSED_OPTIM=0
+    keeps torch's optimizer."""
+    import os
+    from ..fused_optim import ArenaAdam, fusable
+    if os.environ.get("GA_FUSED_OPTIM", "1") != "0" and fusable(spec.cls, spec.kwargs, arena):
+        kw = {k: v for k, v in (spec.kwargs or {}).items() if k in ("lr", "betas", "eps", "weight_decay")}
+        return ArenaAdam(model.parameters(), arena, decoupled=spec.cls is torch.optim.AdamW, **kw)
+    return spec.build(model)
+
+
+def clip_and_step(strategy, max_norm):
+    """clip_grad_norm_(max_norm) (if set) then the inner optimizer step; fused
+    into the ArenaAdam step (norm reduction + device-side coefficient)."""
+    from ..fused_optim import ArenaAdam
+    if isinstance(strategy.optim, ArenaAdam):
+        strategy.optim.step(max_norm=max_norm or None)
+        return
+    if max_norm:
+        strategy.arena.sync_grads()
+        clip_arena_grad_norm_(strategy.arena.grad_flat, max_norm)
+    strategy.optim.step()
 
 
 def clip_arena_grad_norm_(grad_flat, max_norm):
@@ -133,13 +160,11 @@ class SimpleReduceStrategy(Strategy):
         super()._init_node(model, rank, num_nodes)
         arena = self._bind_arena(model)
         self.engine = MeanReduce(self.coll, 1, arena.n, arena.device, arena.dtype)
-        self.optim = self.optim_spec.build(model)
+        self.optim = build_inner_optimizer(self.optim_spec, model, arena)
         self._setup_scheduler()
 
     def step(self):
         self.arena.sync_grads()
         self.engine(self.arena.grad_flat.view(1, -1))
-        if self.max_norm:
-            clip_arena_grad_norm_(self.arena.grad_flat, self.max_norm)
-        self.optim.step()
+        clip_and_step(self, self.max_norm)
         super().step()

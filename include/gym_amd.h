@@ -202,6 +202,41 @@ GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, int32_t nten
                           void* grad, int64_t K, int64_t ld, float lr,
                           hipStream_t stream);
 
+/* ---- inner optimizer on the arena --------------------------------------- */
+
+/* Number of fp32 partials ga_grad_clip_coef needs in its `partials` buffer. */
+GA_API int ga_sumsq_partials_count(void);
+
+/*
+ * Gradient-norm clipping coefficient over a whole gradient arena of n elements:
+ *   out[1] = ||grad||_2 (fp32 partial sums in a fixed order), and
+ *   out[0] = min(1, max_norm / (out[1] + 1e-6)).
+ * Both on the device (nothing synchronises); ga_adam_step applies out[0].
+ * Replaces: torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm) at
+ * exogym/strategy/strategy.py:135-138, communicate_optimize_strategy.py:69-71,
+ * diloco.py:52-56 (the per-tensor norms + stack + norm + per-tensor mul_).
+ */
+GA_API int ga_grad_clip_coef(int dtype, const void* grad, int64_t n, float max_norm, float* partials,
+                             float* out, hipStream_t stream);
+
+/*
+ * One fused Adam/AdamW step over an fp32 arena (param, grad, exp_avg,
+ * exp_avg_sq: n elements each, 16-byte aligned), in torch's op order
+ * (torch/optim/adam.py, _multi_tensor_adam):
+ *   g = grad * clip_coef[0]   (and written back) if clip_coef != null and < 1
+ *   p *= wd_factor            (AdamW: 1 - lr*weight_decay, computed by the caller in double)
+ *   g += l2_wd * p            (Adam with weight_decay)
+ *   m = lerp(m, g, lerp_w)    (lerp_w = 1 - beta1)
+ *   v = beta2*v + one_m_beta2*g*g
+ *   p += step_size * m / (sqrt(v)/bc2_sqrt + eps)   (step_size = -lr/(1-beta1^t), bc2_sqrt = sqrt(1-beta2^t))
+ * Replaces: `self.optim.step()` with the default inner optimizer
+ * torch.optim.AdamW (exogym/strategy/strategy.py:140, diloco.py:59,
+ * communicate_optimize_strategy.py:74; OptimSpec default optim.py:11).
+ */
+GA_API int ga_adam_step(int dtype, void* param, void* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                        float lerp_w, float beta2, float one_m_beta2, float eps, float wd_factor, float l2_wd,
+                        float step_size, float bc2_sqrt, const float* clip_coef, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

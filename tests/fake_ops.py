@@ -131,16 +131,50 @@ def demo_decode(plan, gathered, param, grad, lr):
                 G[k, off:off + nel] = sgn
 
 
+def sumsq_partials(device):
+    return torch.zeros(1024, dtype=torch.float32, device=device)
+
+
+def grad_clip_coef(grad, n, max_norm, partials, out):
+    from oracle import optim as ooptim
+    c, total = ooptim.clip_coef([_np(grad)[:n]], max_norm)
+    out[0] = c
+    out[1] = total
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size,
+              bc2_sqrt, clip_coef=None):
+    """The fused step's arithmetic on CPU tensors (oracle/optim.py order)."""
+    f = np.float32
+    p, g, m, v = _np(param).copy(), _np(grad).copy(), _np(exp_avg).copy(), _np(exp_avg_sq).copy()
+    if clip_coef is not None and float(clip_coef[0]) < 1.0:
+        g = (g * f(float(clip_coef[0]))).astype(f)
+        grad.copy_(torch.from_numpy(g))
+    if wd_factor != 1.0:
+        p = (p * f(wd_factor)).astype(f)
+    if l2_wd != 0.0:
+        g = (g.astype(np.float64) + float(f(l2_wd)) * p.astype(np.float64)).astype(f)
+    m = (m.astype(np.float64) + float(f(lerp_w)) * (g - m).astype(f).astype(np.float64)).astype(f)
+    v = (v * f(beta2)).astype(f)
+    v = (v.astype(np.float64) + (f(one_m_beta2) * g).astype(f).astype(np.float64) * g).astype(f)
+    denom = ((np.sqrt(v).astype(f) / f(bc2_sqrt)).astype(f) + f(eps)).astype(f)
+    p = (p.astype(np.float64) + float(f(step_size)) * (m / denom).astype(f).astype(np.float64)).astype(f)
+    param.copy_(torch.from_numpy(p))
+    exp_avg.copy_(torch.from_numpy(m))
+    exp_avg_sq.copy_(torch.from_numpy(v))
+
+
 def install(monkeypatch_target_modules=None):
     """Point every gym_amd module that imported `ops` at these stand-ins and
     let CPU models through the GPU check."""
     import gym_amd.engine as engine
+    import gym_amd.fused_optim as fused_optim
     import gym_amd.strategy.diloco as diloco
     import gym_amd.strategy.federated_averaging as fedavg
     import gym_amd.strategy.strategy as strategy
     import sys
     me = sys.modules[__name__]
-    for mod in (engine, diloco, fedavg):
+    for mod in (engine, diloco, fedavg, fused_optim):
         mod.ops = me
     strategy.require_gpu = lambda device: None
     import gym_amd.strategy.demo_impl.demo as demo_mod

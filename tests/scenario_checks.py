@@ -120,5 +120,27 @@ def check_engine(res, world, golden_dir, K_local=3):
             np.testing.assert_allclose(res[r]["m_plain"][k], avg, rtol=1e-6, atol=2e-8)
 
 
-CHECKS = {"engine": check_engine, "simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
+def check_simple_adamw(res, world, golden_dir, steps=3):
+    """torch's own pipeline on CPU: mean of the nodes' grads (true division),
+    clip_grad_norm_(0.5), AdamW(lr=3e-3, wd=0.05)."""
+    import torch
+    import strategy_scenarios as S
+    model = S.ShapeModel(S.ADAMW_SHAPES, seed=11)
+    opt = torch.optim.AdamW(model.parameters(), lr=3e-3, weight_decay=0.05)
+    for step in range(steps):
+        per = [S._adamw_grads(r, step, S.ADAMW_SHAPES) for r in range(world)]
+        for i, p in enumerate(model.parameters()):
+            acc = per[0][i].clone()
+            for r in range(1, world):
+                acc += per[r][i]
+            p.grad = acc / world
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 0.5)
+        opt.step()
+    for r in range(world):
+        assert bool(res[r]["fused"]), "the default AdamW should run fused on the arena"
+        for i, p in enumerate(model.parameters()):
+            np.testing.assert_allclose(res[r][f"p_{i}"], p.detach().numpy(), rtol=1e-5, atol=1e-7)
+
+
+CHECKS = {"simple_adamw": check_simple_adamw, "engine": check_engine, "simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
           "sparta_philox": check_sparta_philox, "fedavg": check_fedavg, "demo": check_demo}

@@ -188,6 +188,32 @@ def sc_demo(rank, world, dev, golden_dir):
     return out
 
 
+def _adamw_grads(rank, step, shapes):
+    g = torch.Generator().manual_seed(500 + 97 * rank + step)
+    return [torch.randn(*sh, generator=g) * 0.3 for sh in shapes]
+
+
+ADAMW_SHAPES = [(66, 32), (128,), (3, 7)]
+
+
+def sc_simple_adamw(rank, world, dev, golden_dir, steps=3):
+    """SimpleReduce with the default-class inner optimizer (AdamW, fused on the
+    arena) and gradient clipping: strategy.py:128-142 end to end."""
+    from gym_amd.strategy import OptimSpec, SimpleReduceStrategy
+    model = ShapeModel(ADAMW_SHAPES, seed=11).to(dev)
+    s = SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=3e-3, weight_decay=0.05), max_norm=0.5)
+    s._init_node(model, rank, world)
+    out = {"fused": np.array(type(s.optim).__name__ == "ArenaAdam")}
+    for step in range(steps):
+        s.zero_grad()
+        for p, g in zip(model.parameters(), _adamw_grads(rank, step, ADAMW_SHAPES)):
+            p.grad.copy_(g.to(dev))
+        s.step()
+    for i, p in enumerate(model.parameters()):
+        out[f"p_{i}"] = _host(p)
+    return out
+
+
 def engine_node(j, n, salt=0):
     """Node j's synthetic arena for the batched-replica engine scenario."""
     g = np.random.default_rng(100 + 1000 * salt + j)
@@ -218,7 +244,7 @@ def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4):
     return out
 
 
-SCENARIOS = {"engine": sc_engine, "simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
+SCENARIOS = {"simple_adamw": sc_simple_adamw, "engine": sc_engine, "simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
              "fedavg": sc_fedavg, "demo": sc_demo}
 
 

@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 CASES = [
     ("simple", 2, {}), ("simple", 3, {}), ("simple", 3, {"shard": True, "chunks": 3}),
     ("diloco", 3, {}), ("diloco", 3, {"shard": True}), ("diloco", 3, {"shard": True, "chunks": 5}),
+    ("simple_adamw", 2, {}), ("simple_adamw", 3, {}),
     ("engine", 3, {}),
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": True}),
     ("sparta_philox", 2, {}),

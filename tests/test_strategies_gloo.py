@@ -12,6 +12,7 @@ from scenario_checks import CHECKS
 CASES = [
     ("simple", 2, {}), ("simple", 3, {}), ("simple", 3, {"shard": True, "chunks": 3}),
     ("diloco", 3, {}), ("diloco", 3, {"shard": True}), ("diloco", 3, {"shard": True, "chunks": 5}),
+    ("simple_adamw", 2, {}), ("simple_adamw", 3, {}),
     ("engine", 3, {}), ("engine", 2, {"chunks": 1}),
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": False}),
     ("sparta_philox", 2, {}),
