@@ -78,7 +78,7 @@ class ParamArena:
     buffer and their gradients to another.  Parameters without
     requires_grad are still placed (they keep their values) but get no grad."""
 
-    def __init__(self, params, device=None, dtype=None, world=1, with_grad=True):
+    def __init__(self, params, device=None, dtype=None, world=1, with_grad=True, flat=None, grad_flat=None):
         self.params = [p for p in params]
         if not self.params:
             raise ValueError("ParamArena: empty parameter list")
@@ -89,8 +89,13 @@ class ParamArena:
                 raise TypeError(f"ParamArena: mixed parameter dtypes ({p.dtype} vs {self.dtype})")
         self.layout = ArenaLayout([p.shape for p in self.params])
         n = self.layout.padded_to(world)
-        self.flat = torch.zeros(n, device=self.device, dtype=self.dtype)
-        self.grad_flat = torch.zeros(n, device=self.device, dtype=self.dtype) if with_grad else None
+        if flat is not None:  # a row of a ReplicaArena (zeroed by its owner)
+            if flat.numel() != n or (with_grad and (grad_flat is None or grad_flat.numel() != n)):
+                raise ValueError(f"ParamArena: external buffers must hold {n} elements")
+            self.flat, self.grad_flat = flat, (grad_flat if with_grad else None)
+        else:
+            self.flat = torch.zeros(n, device=self.device, dtype=self.dtype)
+            self.grad_flat = torch.zeros(n, device=self.device, dtype=self.dtype) if with_grad else None
         with torch.no_grad():
             for p, v in zip(self.params, self.layout.views(self.flat)):
                 v.copy_(p.data)
@@ -137,6 +142,57 @@ class ParamArena:
     def zero_grad(self):
         if self.grad_flat is not None:
             self.grad_flat.zero_()
+            self.rebind_grads()
+
+    def rebind_grads(self):
+        """Point every trainable parameter's .grad back at its arena view."""
+        if self._grad_views is not None:
             for p, g in zip(self.params, self._grad_views):
                 if p.requires_grad:
                     p.grad = g
+
+
+class ReplicaArena:
+    """K simulated nodes hosted by one process (batched-replica mode,
+    SURVEY §8(f) row 1): K model copies whose parameters and gradients are the
+    rows of one [K, ld] parameter set and one [K, ld] gradient set, so every
+    strategy kernel covers all K nodes in one launch.  arenas[k] is node k's
+    ParamArena (row views; model k's param.data / .grad point into them)."""
+
+    def __init__(self, models, world=1, with_grad=True):
+        self.models = list(models)
+        if not self.models:
+            raise ValueError("ReplicaArena: no models")
+        p0 = list(self.models[0].parameters())
+        self.layout = ArenaLayout([p.shape for p in p0])
+        self.K = len(self.models)
+        self.ld = self.layout.padded_to(world)
+        self.device, self.dtype = p0[0].device, p0[0].dtype
+        self.flat_set = torch.zeros(self.K, self.ld, device=self.device, dtype=self.dtype)
+        self.grad_set = torch.zeros(self.K, self.ld, device=self.device, dtype=self.dtype) if with_grad else None
+        self.arenas = []
+        for k, m in enumerate(self.models):
+            ps = list(m.parameters())
+            if [tuple(p.shape) for p in ps] != self.layout.shapes:
+                raise ValueError("ReplicaArena: the replicas must share one parameter layout")
+            self.arenas.append(ParamArena(ps, world=world, with_grad=with_grad, flat=self.flat_set[k],
+                                          grad_flat=self.grad_set[k] if with_grad else None))
+        self.params = [p for a in self.arenas for p in a.params]
+
+    @property
+    def n(self):
+        return self.ld
+
+    def sync_grads(self):
+        for a in self.arenas:
+            a.sync_grads()
+
+    def zero_grad(self):
+        if self.grad_set is not None:
+            self.grad_set.zero_()
+            for a in self.arenas:
+                a.rebind_grads()
+
+    def check_bound(self):
+        for a in self.arenas:
+            a.check_bound()

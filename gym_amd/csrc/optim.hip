@@ -41,8 +41,14 @@ __device__ __forceinline__ void adam_elem(float& p, float& g, float& m, float& v
 
 __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ param, float* __restrict__ grad,
                                                          float* __restrict__ m_, float* __restrict__ v_, int64_t n,
-                                                         AdamParams ap, const float* __restrict__ clip_coef) {
-    const float coef = clip_coef ? *clip_coef : 1.f;
+                                                         int64_t ld, AdamParams ap,
+                                                         const float* __restrict__ clip_coef) {
+    const int64_t rep = blockIdx.y;  // replica (simulated node) of a [K, ld] set
+    param += rep * ld;
+    grad += rep * ld;
+    m_ += rep * ld;
+    v_ += rep * ld;
+    const float coef = clip_coef ? clip_coef[2 * rep] : 1.f;
     const bool scale = coef < 1.f;
     const int64_t nv = n >> 2;
     const int64_t lo = (int64_t)blockIdx.x * kOptChunk;
@@ -82,9 +88,11 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ par
 
 // partials[b] = sum of x^2 over a grid-stride share of the arena (fp32, fixed order)
 template <typename T>
-__global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const T* __restrict__ x, int64_t n,
+__global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const T* __restrict__ x, int64_t n, int64_t ld,
                                                           float* __restrict__ partials) {
     __shared__ float red[kOptBlock / 64];
+    x += (int64_t)blockIdx.y * ld;
+    partials += (int64_t)blockIdx.y * gridDim.x;
     float acc = 0.f;
     const int64_t stride = (int64_t)gridDim.x * kOptBlock;
     const int64_t nv = ((uintptr_t)x % (4 * sizeof(T)) == 0) ? n / 4 : 0;  // 4-element vectors
@@ -111,6 +119,8 @@ __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const T* __restrict__ 
 __global__ __launch_bounds__(kOptBlock) void clip_coef_kernel(const float* __restrict__ partials, int np,
                                                               float max_norm, float* __restrict__ out) {
     __shared__ float red[kOptBlock / 64];
+    partials += (int64_t)blockIdx.x * np;  // one workgroup per replica
+    out += 2 * (int64_t)blockIdx.x;
     float acc = 0.f;
     for (int i = threadIdx.x; i < np; i += kOptBlock) acc += partials[i];
 #pragma unroll
@@ -131,36 +141,40 @@ using namespace ga;
 
 extern "C" GA_API int ga_sumsq_partials_count(void) { return kSumsqBlocks; }
 
-extern "C" GA_API int ga_grad_clip_coef(int dtype, const void* grad, int64_t n, float max_norm, float* partials,
-                                        float* out, hipStream_t stream) {
+extern "C" GA_API int ga_grad_clip_coef(int dtype, const void* grad, int64_t K, int64_t ld, int64_t n,
+                                        float max_norm, float* partials, float* out, hipStream_t stream) {
     clear_error();
-    GA_REQUIRE(n >= 0, "ga_grad_clip_coef: n < 0");
+    GA_REQUIRE(n >= 0 && K >= 1 && K <= 65535, "ga_grad_clip_coef: bad sizes n=%lld K=%lld", (long long)n,
+               (long long)K);
+    GA_REQUIRE(K == 1 || ld >= n, "ga_grad_clip_coef: ld < n");
     GA_REQUIRE(grad && partials && out, "ga_grad_clip_coef: null buffer");
     GA_REQUIRE(max_norm > 0.f, "ga_grad_clip_coef: max_norm must be > 0");
     const int blocks = kSumsqBlocks;
     switch (dtype) {
         case GA_F32:
-            hipLaunchKernelGGL(sumsq_kernel<float>, dim3(blocks), dim3(kOptBlock), 0, stream, (const float*)grad, n,
-                               partials);
+            hipLaunchKernelGGL(sumsq_kernel<float>, dim3(blocks, (unsigned)K), dim3(kOptBlock), 0, stream,
+                               (const float*)grad, n, ld, partials);
             break;
         case GA_BF16:
-            hipLaunchKernelGGL(sumsq_kernel<__hip_bfloat16>, dim3(blocks), dim3(kOptBlock), 0, stream,
-                               (const __hip_bfloat16*)grad, n, partials);
+            hipLaunchKernelGGL(sumsq_kernel<__hip_bfloat16>, dim3(blocks, (unsigned)K), dim3(kOptBlock), 0, stream,
+                               (const __hip_bfloat16*)grad, n, ld, partials);
             break;
         default: set_error("ga_grad_clip_coef: unknown dtype %d", dtype); return GA_EINVAL;
     }
     if (int e = check_launch("ga_grad_clip_coef (sumsq)")) return e;
-    hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(kOptBlock), 0, stream, partials, blocks, max_norm, out);
+    hipLaunchKernelGGL(clip_coef_kernel, dim3((unsigned)K), dim3(kOptBlock), 0, stream, partials, blocks, max_norm,
+                       out);
     return check_launch("ga_grad_clip_coef");
 }
 
-extern "C" GA_API int ga_adam_step(int dtype, void* param, void* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-                                   float lerp_w, float beta2, float one_m_beta2, float eps, float wd_factor,
-                                   float l2_wd, float step_size, float bc2_sqrt, const float* clip_coef,
-                                   hipStream_t stream) {
+extern "C" GA_API int ga_adam_step(int dtype, void* param, void* grad, float* exp_avg, float* exp_avg_sq, int64_t K,
+                                   int64_t ld, int64_t n, float lerp_w, float beta2, float one_m_beta2, float eps,
+                                   float wd_factor, float l2_wd, float step_size, float bc2_sqrt,
+                                   const float* clip_coef, hipStream_t stream) {
     clear_error();
-    GA_REQUIRE(n >= 0, "ga_adam_step: n < 0");
+    GA_REQUIRE(n >= 0 && K >= 1 && K <= 65535, "ga_adam_step: bad sizes n=%lld K=%lld", (long long)n, (long long)K);
     if (n == 0) return GA_OK;
+    GA_REQUIRE(K == 1 || (ld >= n && ld % 4 == 0), "ga_adam_step: ld must be >= n and a multiple of 4");
     GA_REQUIRE(param && grad && exp_avg && exp_avg_sq, "ga_adam_step: null buffer");
     GA_REQUIRE(dtype == GA_F32, "ga_adam_step: only float32 arenas are fused (dtype %d)", dtype);
     GA_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
@@ -170,7 +184,7 @@ extern "C" GA_API int ga_adam_step(int dtype, void* param, void* grad, float* ex
     const int64_t nv = n / 4;
     int64_t grid = (nv + kOptChunk - 1) / kOptChunk;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)grid), dim3(kOptBlock), 0, stream, (float*)param, (float*)grad,
-                       exp_avg, exp_avg_sq, n, ap, clip_coef);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)grid, (unsigned)K), dim3(kOptBlock), 0, stream, (float*)param,
+                       (float*)grad, exp_avg, exp_avg_sq, n, ld, ap, clip_coef);
     return check_launch("ga_adam_step");
 }

@@ -28,7 +28,8 @@ def fusable(spec_cls, kwargs, arena):
     """True when OptimSpec(spec_cls, **kwargs) can run as ArenaAdam on this arena."""
     if spec_cls not in (torch.optim.AdamW, torch.optim.Adam):
         return False
-    if arena is None or arena.grad_flat is None or arena.dtype != torch.float32:
+    grads = getattr(arena, "grad_set", None) if hasattr(arena, "grad_set") else getattr(arena, "grad_flat", None)
+    if arena is None or grads is None or arena.dtype != torch.float32:
         return False
     kw = dict(kwargs or {})
     if any(kw.get(k) for k in _UNSUPPORTED):
@@ -43,6 +44,10 @@ def fusable(spec_cls, kwargs, arena):
 
 
 class ArenaAdam(torch.optim.Optimizer):
+    """Adam/AdamW over one node's ParamArena, or over a ReplicaArena (K nodes of
+    one process, [K, ld] parameter/gradient sets: one launch for all of them,
+    each replica clipped by its own gradient norm)."""
+
     def __init__(self, params, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=None, decoupled=True,
                  **ignored):
         if weight_decay is None:
@@ -62,31 +67,38 @@ class ArenaAdam(torch.optim.Optimizer):
         super().__init__(params, defaults)
         if len(self.param_groups) != 1:
             raise ValueError("ArenaAdam: one parameter group (the node's arena)")
-        self.arena = arena
-        dev = arena.flat.device
-        self.exp_avg = torch.zeros(arena.n, dtype=torch.float32, device=dev)
-        self.exp_avg_sq = torch.zeros(arena.n, dtype=torch.float32, device=dev)
+        self.arenas = list(getattr(arena, "arenas", [arena]))
+        self.P = arena.flat_set if hasattr(arena, "flat_set") else arena.flat.view(1, -1)
+        self.G = arena.grad_set if hasattr(arena, "grad_set") else arena.grad_flat.view(1, -1)
+        self.K, self.ld = self.P.shape
+        dev = self.P.device
+        self.M = torch.zeros_like(self.P, dtype=torch.float32)
+        self.V = torch.zeros_like(self.P, dtype=torch.float32)
+        self.exp_avg, self.exp_avg_sq = self.M.view(-1), self.V.view(-1)  # flat views (single-arena users)
         self._step_t = torch.tensor(0.0)
-        index = {id(p): i for i, p in enumerate(arena.params)}
-        self._spans = []  # (param, arena offset, numel) in arena order
+        where = {}
+        for k, ar in enumerate(self.arenas):
+            for i, p in enumerate(ar.params):
+                where[id(p)] = (k, ar.layout.offsets[i], ar.layout.numels[i])
+        self._spans = [[] for _ in self.arenas]  # per replica: (param, offset, numel) in arena order
         for p in self.param_groups[0]["params"]:
-            if id(p) not in index:
+            if id(p) not in where:
                 raise ValueError("ArenaAdam: every parameter must live in the arena")
-            i = index[id(p)]
-            o, n = arena.layout.offsets[i], arena.layout.numels[i]
-            self._spans.append((p, o, n))
-            self.state[p] = {"step": self._step_t, "exp_avg": self.exp_avg[o:o + n].view(p.shape),
-                             "exp_avg_sq": self.exp_avg_sq[o:o + n].view(p.shape)}
-        self._spans.sort(key=lambda s: s[1])
-        self._partials = ops.sumsq_partials(dev)
-        self._clip = torch.ones(2, dtype=torch.float32, device=dev)
+            k, o, n = where[id(p)]
+            self._spans[k].append((p, o, n))
+            self.state[p] = {"step": self._step_t, "exp_avg": self.M[k, o:o + n].view(p.shape),
+                             "exp_avg_sq": self.V[k, o:o + n].view(p.shape)}
+        for sp in self._spans:
+            sp.sort(key=lambda t: t[1])
+        self._partials = ops.sumsq_partials(dev, self.K)
+        self._clip = torch.ones(2 * self.K, dtype=torch.float32, device=dev)
 
-    def _ranges(self):
-        """Contiguous arena ranges [a, b) of the parameters that have a gradient
-        now (a whole-arena range when all do, padding included: it stays 0)."""
-        live = [(o, n) for p, o, n in self._spans if p.grad is not None]
-        if len(live) == len(self._spans):
-            return [(0, self.arena.n)]
+    def _ranges(self, k):
+        """Contiguous ranges [a, b) of replica k's arena whose parameters have a
+        gradient now (the whole row when all do: the padding stays 0)."""
+        live = [(o, n) for p, o, n in self._spans[k] if p.grad is not None]
+        if len(live) == len(self._spans[k]):
+            return [(0, self.ld)]
         out = []
         for o, n in live:
             if out and o - out[-1][1] < 64:  # adjacent tensors (the alignment gap is zero padding)
@@ -101,8 +113,9 @@ class ArenaAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        ranges = self._ranges()
-        self.arena.sync_grads()
+        ranges = [self._ranges(k) for k in range(self.K)]
+        for ar in self.arenas:
+            ar.sync_grads()
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = float(g["lr"]), g["betas"], float(g["eps"]), float(g["weight_decay"])
         decoupled = g["decoupled_weight_decay"]
@@ -110,15 +123,18 @@ class ArenaAdam(torch.optim.Optimizer):
         t = float(self._step_t)
         bc1 = 1 - b1 ** t
         bc2 = 1 - b2 ** t
-        step_size = -(lr / bc1)
-        bc2_sqrt = math.sqrt(bc2)
-        wd_factor = (1 - lr * wd) if (decoupled and wd != 0) else 1.0
-        l2 = wd if (not decoupled and wd != 0) else 0.0
+        hp = dict(lerp_w=1 - b1, beta2=b2, one_m_beta2=1 - b2, eps=eps,
+                  wd_factor=(1 - lr * wd) if (decoupled and wd != 0) else 1.0,
+                  l2_wd=wd if (not decoupled and wd != 0) else 0.0, step_size=-(lr / bc1), bc2_sqrt=math.sqrt(bc2))
         clip = None
         if max_norm:
-            ops.grad_clip_coef(self.arena.grad_flat, self.arena.n, max_norm, self._partials, self._clip)
+            ops.grad_clip_coef(self.G, self.ld, max_norm, self._partials, self._clip)
             clip = self._clip
-        for a, b in ranges:
-            ops.adam_step(self.arena.flat[a:b], self.arena.grad_flat[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
-                          1 - b1, b2, 1 - b2, eps, wd_factor, l2, step_size, bc2_sqrt, clip)
+        if all(r == [(0, self.ld)] for r in ranges):
+            ops.adam_step(self.P, self.G, self.M, self.V, clip_coef=clip, **hp)
+            return loss
+        for k in range(self.K):
+            ck = clip[2 * k:2 * k + 2] if clip is not None else None
+            for a, b in ranges[k]:
+                ops.adam_step(self.P[k, a:b], self.G[k, a:b], self.M[k, a:b], self.V[k, a:b], clip_coef=ck, **hp)
         return loss

@@ -195,30 +195,38 @@ def demo_decode(plan, gathered, param, grad, lr):
           "ga_demo_decode")
 
 
-def sumsq_partials(device):
-    return torch.empty(int(lib().ga_sumsq_partials_count()), dtype=torch.float32, device=device)
+def sumsq_partials(device, K=1):
+    return torch.empty(int(K) * int(lib().ga_sumsq_partials_count()), dtype=torch.float32, device=device)
 
 
 def grad_clip_coef(grad, n, max_norm, partials, out):
-    """out[0] <- min(1, max_norm / (||grad[:n]||_2 + 1e-6)), out[1] <- the norm (device side)."""
-    _gpu(grad, partials, out)
-    if partials.numel() < lib().ga_sumsq_partials_count() or out.numel() < 2 or out.dtype != torch.float32:
+    """Per replica k of grad ([K, ld] set or 1-D): out[2k] <- min(1, max_norm /
+    (||grad_k[:n]||_2 + 1e-6)), out[2k+1] <- the norm (device side)."""
+    g2 = _as2d(grad)
+    _gpu(g2, partials, out)
+    K, ld = _rows_ld(g2)
+    if partials.numel() < K * lib().ga_sumsq_partials_count() or out.numel() < 2 * K or out.dtype != torch.float32:
         raise ValueError("grad_clip_coef: partials/out too small")
-    check(lib().ga_grad_clip_coef(_dtype_code(grad), _p(grad), int(n), float(max_norm), _p(partials), _p(out),
+    check(lib().ga_grad_clip_coef(_dtype_code(g2), _p(g2), K, ld, int(n), float(max_norm), _p(partials), _p(out),
                                   _stream()), "ga_grad_clip_coef")
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size,
-              bc2_sqrt, clip_coef=None):
-    """One fused Adam/AdamW step over fp32 flat buffers of equal length (see include/gym_amd.h)."""
-    _gpu(param, grad, exp_avg, exp_avg_sq, clip_coef)
-    n = param.numel()
-    for t in (grad, exp_avg, exp_avg_sq):
-        if t.numel() != n or t.dtype != torch.float32 or not t.is_contiguous():
-            raise ValueError("adam_step: param/grad/exp_avg/exp_avg_sq must be contiguous fp32 of one length")
-    if param.dtype != torch.float32 or not param.is_contiguous():
-        raise TypeError("adam_step: fused path is fp32 only")
-    check(lib().ga_adam_step(_dtype_code(param), _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), n,
-                             float(lerp_w), float(beta2), float(one_m_beta2), float(eps), float(wd_factor),
-                             float(l2_wd), float(step_size), float(bc2_sqrt), _p(clip_coef), _stream()),
-          "ga_adam_step")
+              bc2_sqrt, clip_coef=None, n=None):
+    """One fused Adam/AdamW step over fp32 [K, ld] replica sets (or 1-D buffers)
+    of one shape; every replica's first n elements (see include/gym_amd.h)."""
+    ts = [_as2d(t) for t in (param, grad, exp_avg, exp_avg_sq)]
+    _gpu(*ts, clip_coef)
+    K, ld = _rows_ld(ts[0])
+    for t in ts:
+        if t.dtype != torch.float32 or t.shape != ts[0].shape or t.stride() != ts[0].stride() or t.stride(-1) != 1:
+            raise ValueError("adam_step: param/grad/exp_avg/exp_avg_sq must be fp32 replica sets of one layout")
+    n = ts[0].shape[1] if n is None else int(n)
+    if clip_coef is not None and clip_coef.numel() < 2 * K:
+        raise ValueError("adam_step: clip_coef must hold 2 floats per replica")
+    check(lib().ga_adam_step(_GA_F32, _p(ts[0]), _p(ts[1]), _p(ts[2]), _p(ts[3]), K, ld, n, float(lerp_w),
+                             float(beta2), float(one_m_beta2), float(eps), float(wd_factor), float(l2_wd),
+                             float(step_size), float(bc2_sqrt), _p(clip_coef), _stream()), "ga_adam_step")
+
+
+_GA_F32 = _lib.GA_F32

@@ -1,0 +1,333 @@
+"""Batched-replica node loop.
+
+The reference runs one OS process per simulated node and, with more nodes than
+GPUs, puts several processes on one GPU over gloo (exogym/trainer.py:310-351).
+Here one process per GPU hosts K_local = num_nodes / processes simulated nodes:
+K model copies whose parameters and gradients are the rows of one [K, ld]
+ReplicaArena, so the strategy's communication step is the batched engine
+(gym_amd.engine: in-kernel reduction over the K local nodes, RCCL across the
+processes) and the inner optimizer is one fused launch over all K nodes.
+
+Each node keeps the reference's per-node semantics (train_node.py:145-175):
+its own data shard (DistributedSampler(num_replicas=num_nodes, rank=node) or
+the dataset factory called with the node's rank), gradient accumulation over
+batch_size // minibatch_size minibatches with `grad /= batch_size /
+minibatch_size`, its own clip_grad_norm_, then the strategy step.  Supported
+strategies: SimpleReduce, DiLoCo (SGD-family outer optimizer), SPARTA (Philox
+mask stream), FedAvg without islands, DeMo.  Anything else runs on the
+process-per-node path (ReplicaRunner.supports).
+"""
+import copy
+
+import numpy as np
+import torch
+import torch.distributed as dist
+from torch.utils.data import DataLoader
+
+from . import ops
+from .arena import ReplicaArena
+from .comm import Collective
+from .engine import DeMoCodec, DiLoCoOuter, MeanReduce, Sparta
+from .fused_optim import ArenaAdam, fusable
+from .strategy.demo import DeMoStrategy
+from .strategy.diloco import DiLoCoStrategy, fused_sgd_hparams
+from .strategy.federated_averaging import FedAvgStrategy
+from .strategy.sparta import RandomIndexSelector, SPARTAStrategy
+from .strategy.strategy import SimpleReduceStrategy, clip_arena_grad_norm_
+
+
+class _LRGroup(torch.optim.Optimizer):
+    """Holds the learning rate a scheduler drives when the step itself is a
+    kernel (DeMo): one group with one placeholder parameter, no state."""
+
+    def __init__(self, lr):
+        super().__init__([torch.zeros(1, requires_grad=True)], {"lr": lr})
+
+    def step(self, closure=None):
+        return None
+
+
+class _PerNodeOptim:
+    """K torch optimizers (a non-fusable inner OptimSpec), one per local node,
+    each clipped by its own gradient norm (clip_grad_norm_ per node)."""
+
+    def __init__(self, spec, models, arenas):
+        self.opts = [spec.build(m) for m in models]
+        self.arenas = arenas
+        self.param_groups = self.opts[0].param_groups
+
+    def step(self, max_norm=None):
+        for a, o in zip(self.arenas, self.opts):
+            if max_norm:
+                a.sync_grads()
+                clip_arena_grad_norm_(a.grad_flat, max_norm)
+            o.step()
+
+
+class ReplicaRunner:
+    """The strategy step for the K_local nodes of one process."""
+
+    @staticmethod
+    def supports(strategy):
+        if isinstance(strategy, SPARTAStrategy):
+            sel = strategy.index_selector
+            return isinstance(sel, RandomIndexSelector) and sel.mask_source == "philox"
+        if isinstance(strategy, FedAvgStrategy):
+            return strategy.island_size is None
+        if isinstance(strategy, DiLoCoStrategy):
+            return fused_sgd_hparams(strategy.outer_optim_spec) is not None
+        return isinstance(strategy, (SimpleReduceStrategy, DeMoStrategy))
+
+    def __init__(self, strategy, models, rank, num_nodes):
+        if not self.supports(strategy):
+            raise NotImplementedError(f"{type(strategy).__name__} with these options has no batched-replica path")
+        self.s = strategy
+        self.coll = Collective()
+        self.K = len(models)
+        self.rank, self.num_nodes = rank, num_nodes
+        self.first_node = rank * self.K
+        if self.coll.world * self.K != num_nodes:
+            raise ValueError(f"{self.coll.world} processes x {self.K} replicas != {num_nodes} nodes")
+        self.models = models
+        self.ra = ReplicaArena(models, world=self.coll.world)
+        dev, dt, ld = self.ra.device, self.ra.dtype, self.ra.ld
+        # every node starts from node 0's parameters (train_node.py:86-92)
+        with torch.no_grad():
+            self.coll.broadcast_(self.ra.flat_set[0], 0)
+            if self.K > 1:
+                ops.replica_mean(self.ra.flat_set[0:1], self.ra.flat_set[1:], divisor=1.0)
+        s = strategy
+        s.local_step = 0
+        s.max_steps = getattr(s, "max_steps", 1)
+        s.rank, s.num_nodes = rank, num_nodes
+        self.max_norm = None
+        self.lr_scheds = []
+        if isinstance(s, DeMoStrategy):
+            self.optim = _LRGroup(s.kwargs.get("lr", 0.001))
+            self.delta = torch.zeros_like(self.ra.flat_set)
+            self.codec = DeMoCodec(self.coll, self.K, self.ra.layout, dev, chunk=s.compression_chunk,
+                                   topk=s.compression_topk)
+        else:
+            spec = s.optim_spec if isinstance(s, SimpleReduceStrategy) else s.inner_optim_spec
+            if fusable(spec.cls, spec.kwargs, self.ra):
+                kw = {k: v for k, v in (spec.kwargs or {}).items() if k in ("lr", "betas", "eps", "weight_decay")}
+                self.optim = ArenaAdam(self.ra.params, self.ra, decoupled=spec.cls is torch.optim.AdamW, **kw)
+            else:
+                self.optim = _PerNodeOptim(spec, models, self.ra.arenas)
+            if isinstance(s, DiLoCoStrategy):
+                self.max_norm = s.kwargs.get("max_norm")
+                self.outer = DiLoCoOuter(self.coll, self.K, ld, dev, dt, **fused_sgd_hparams(s.outer_optim_spec))
+                self.outer.init_master(self.ra.flat_set[0])
+            else:
+                self.max_norm = s.max_norm
+            if isinstance(s, (SimpleReduceStrategy, FedAvgStrategy)):
+                self.mean = MeanReduce(self.coll, self.K, ld, dev, dt)
+            elif isinstance(s, SPARTAStrategy):
+                self.sparta = Sparta(self.coll, self.K, ld, dev, dt, s.index_selector.p)
+                t = torch.tensor([torch.initial_seed() & (2**63 - 1)], dtype=torch.int64, device=dev)
+                self.coll.broadcast_(t, 0)
+                self.seed = int(t.item())
+                self.iteration = 0
+        # the strategy's LR schedule on every optimizer (strategy.py:75-112)
+        for o in (self.optim.opts if isinstance(self.optim, _PerNodeOptim) else [self.optim]):
+            s.optim = o
+            s._setup_scheduler()
+            if s.scheduler is not None:
+                self.lr_scheds.append(s.scheduler)
+        s.optim = self.optim
+
+    def zero_grad(self):
+        self.ra.zero_grad()
+
+    @torch.no_grad()
+    def step(self):
+        s = self.s
+        self.ra.check_bound()
+        P, G = self.ra.flat_set, self.ra.grad_set
+        if isinstance(s, DeMoStrategy):
+            self.ra.sync_grads()
+            lr = self.optim.param_groups[0]["lr"]
+            self.codec(P, G, self.delta, lr, s.compression_decay, s.weight_decay)
+        elif isinstance(s, SimpleReduceStrategy):
+            self.ra.sync_grads()
+            self.mean(G)
+            self._inner()
+        elif isinstance(s, DiLoCoStrategy):
+            self._inner()
+            if s.local_step % s.H == 0 and s.local_step > 0:
+                self.outer(P)
+        elif isinstance(s, SPARTAStrategy):
+            self._inner()
+            self.sparta(P, seed=self.seed, iteration=self.iteration)
+            self.iteration += 1
+        elif isinstance(s, FedAvgStrategy):
+            self._inner()
+            if s.local_step % s.H == 0 and s.local_step > 0:
+                self.mean(P)
+        for sch in self.lr_scheds:
+            sch.step()
+        if self.rank == 0 and self.lr_scheds:
+            for cb in s.lr_callbacks:
+                cb(self.lr_scheds[0].get_last_lr()[0])
+        s.local_step += 1
+
+    def _inner(self):
+        if isinstance(self.optim, ArenaAdam):
+            self.optim.step(max_norm=self.max_norm or None)
+        else:
+            self.optim.step(max_norm=self.max_norm)
+
+    def averaged_flat(self):
+        """The mean over all num_nodes nodes' parameters (a new [ld] buffer)."""
+        avg = torch.empty(self.ra.ld, device=self.ra.device, dtype=self.ra.dtype)
+        ops.replica_mean(self.ra.flat_set, avg, divisor=1.0)
+        self.coll.all_reduce_(avg)
+        ops.replica_mean(avg, avg, divisor=float(self.num_nodes))
+        return avg
+
+
+class ReplicaTrainNode:
+    """TrainNode (train_node.py:19-626) for the K_local nodes of one process."""
+
+    def __init__(self, model, train_dataset, val_dataset, strategy, device, rank, num_nodes, K, num_epochs,
+                 max_steps=None, batch_size=16, minibatch_size=16, val_size=64, val_interval=100, shuffle=True,
+                 autocast=False, **kwargs):
+        from .train_node import RunLog
+        seed = kwargs.get("seed", 42)
+        torch.manual_seed(seed)
+        torch.cuda.manual_seed(seed)
+        np.random.seed(seed)
+        self.device, self.rank, self.num_nodes, self.K = device, rank, num_nodes, K
+        self.models = [copy.deepcopy(model).to(device) for _ in range(K)]
+        self.nodes = [rank * K + k for k in range(K)]
+        self.batch_size, self.minibatch_size = batch_size, minibatch_size
+        self.val_size, self.val_interval, self.autocast = val_size, val_interval, autocast
+        self.loaders, self.iters, self.epoch = [], [], 0
+        for node in self.nodes:
+            if callable(train_dataset):
+                ds, sampler = train_dataset(node, num_nodes, False), None
+            else:
+                ds = train_dataset
+                sampler = torch.utils.data.DistributedSampler(ds, num_replicas=num_nodes, rank=node, shuffle=shuffle)
+            dl = DataLoader(ds, batch_size=minibatch_size, sampler=sampler, shuffle=(sampler is None))
+            self.loaders.append(dl)
+            self.iters.append(iter(dl))
+        vds = val_dataset(self.nodes[0], num_nodes, True) if callable(val_dataset) else val_dataset
+        self.val_loader = DataLoader(vds, batch_size=minibatch_size, shuffle=True)
+        self.val_iter = iter(self.val_loader)
+        torch.manual_seed(42)
+        torch.cuda.manual_seed(42)
+        self.runner = ReplicaRunner(strategy, self.models, rank, num_nodes)
+        self.strategy = strategy
+        if max_steps is None:
+            max_steps = num_epochs * len(self.loaders[0]) / (batch_size // minibatch_size)
+        self.max_steps = max_steps
+        strategy.max_steps = max_steps
+        self.local_step = 0
+        self.logger = RunLog(strategy, max_steps) if rank == 0 else None
+
+    def _next(self, k):
+        try:
+            batch = next(self.iters[k])
+        except StopIteration:
+            if k == 0:
+                self.epoch += 1
+            self.iters[k] = iter(self.loaders[k])
+            batch = next(self.iters[k])
+        return self._to(batch)
+
+    def _next_val(self):
+        try:
+            batch = next(self.val_iter)
+        except StopIteration:
+            self.val_iter = iter(self.val_loader)
+            batch = next(self.val_iter)
+        return self._to(batch)
+
+    def _to(self, batch):
+        if isinstance(batch, (tuple, list)):
+            return tuple(x.to(self.device) for x in batch)
+        return batch.to(self.device)
+
+    def _forward(self, model, minibatch):
+        if self.autocast:
+            with torch.autocast(device_type=torch.device(self.device).type, dtype=torch.bfloat16):
+                return model(minibatch)
+        return model(minibatch)
+
+    def _train_step(self):
+        self.runner.zero_grad()
+        accum = self.batch_size // self.minibatch_size
+        loss0 = None
+        for k, m in enumerate(self.models):
+            for _ in range(accum):
+                loss = self._forward(m, self._next(k))
+                loss.backward()
+                if k == 0:
+                    loss0 = loss
+        self.runner.ra.sync_grads()
+        self.runner.ra.grad_set.div_(self.batch_size / self.minibatch_size)
+        self.runner.step()
+        if self.logger is not None:
+            self.logger.log_train(loss=loss0.item())
+
+    def _eval_loss(self, model):
+        model.eval()
+        total = 0.0
+        accum = self.batch_size // self.minibatch_size
+        with torch.no_grad():
+            for _ in range(int(self.val_size / self.batch_size)):
+                for _ in range(accum):
+                    total += self._forward(model, self._next_val()).item() / accum
+        model.train()
+        return total / max(1, int(self.val_size / self.batch_size))
+
+    def _evaluate(self):
+        if self.val_size == 0:
+            return
+        avg = self.runner.averaged_flat() if self.num_nodes > 1 else None
+        if self.rank != 0:
+            return
+        self.logger.log_loss(loss=self._eval_loss(self.models[0]), name="local")
+        if avg is not None:
+            clone = copy.deepcopy(self.models[0])
+            with torch.no_grad():
+                for p, v in zip(clone.parameters(), self.runner.ra.layout.views(avg)):
+                    p.copy_(v)
+            self.logger.log_loss(loss=self._eval_loss(clone), name="global")
+
+    def train(self):
+        world = self.runner.coll.world
+        while self.local_step < self.max_steps:
+            if self.local_step % self.val_interval == 0:
+                self._evaluate()
+            self._train_step()
+            self.local_step += 1
+            if self.logger is not None:
+                self.logger.increment_step()
+            if world > 1:
+                dist.barrier()
+        self._evaluate()
+        return [m.state_dict() for m in self.models]
+
+
+def replica_layout(num_nodes, devices, replicas_per_process, strategy):
+    """(processes, K_local) for Trainer.fit, or None for the process-per-node
+    path.  replicas_per_process: None/"auto" = batch the nodes when there are
+    more nodes than GPUs; an int forces K_local (1 = process per node)."""
+    if replicas_per_process in (None, "auto"):
+        G = len(devices)
+        if num_nodes <= G or num_nodes % G != 0 or not ReplicaRunner.supports(strategy):
+            return None
+        return G, num_nodes // G
+    K = int(replicas_per_process)
+    if K <= 1:
+        return None
+    if num_nodes % K != 0:
+        raise ValueError(f"num_nodes={num_nodes} is not a multiple of replicas_per_process={K}")
+    if not ReplicaRunner.supports(strategy):
+        raise NotImplementedError(f"{type(strategy).__name__} with these options has no batched-replica path")
+    G = num_nodes // K
+    if G > len(devices):
+        raise ValueError(f"{G} processes need {G} GPUs, {len(devices)} given")
+    return G, K

@@ -12,10 +12,11 @@ Process-group setup (the north star's "process-group setup in trainer.py"):
     is "nccl", i.e. RCCL over xGMI on ROCm, node i on devices[i]; the strategies
     then run their flat-arena collectives (reduce-scatter / all-gather /
     all-reduce) over RCCL;
-  - more nodes than GPUs: nodes share GPUs round-robin over a gloo group (RCCL
-    cannot put two ranks on one GPU); the strategies use their all-reduce
-    paths.  (Batched replicas inside one process are the faster way to run
-    K > 8 nodes; see gym_amd.engine and bench.py.)
+  - more nodes than GPUs (and a multiple of them): one process per GPU hosts
+    num_nodes / GPUs simulated nodes on a [K, ld] replica arena
+    (gym_amd.replica, replicas_per_process="auto"), RCCL across the GPUs;
+  - otherwise (or replicas_per_process=1) nodes share GPUs round-robin over a
+    gloo group (RCCL cannot put two ranks on one GPU).
   - MASTER_ADDR is 127.0.0.1; device "cpu"/"mps" is refused (the step kernels
     are MI355X kernels, there is no CPU path).
 The final average of the nodes' state dicts (trainer.py:95-119) runs on the GPU
@@ -76,6 +77,28 @@ def _worker(rank: int, config: TrainingConfig, result_queue):
     result_queue.put((rank, OrderedDict((k, v.detach().cpu()) for k, v in state.items())))
 
 
+def _replica_worker(rank: int, config: TrainingConfig, procs: int, K: int, result_queue):
+    """One process per GPU hosting K simulated nodes (gym_amd.replica)."""
+    from .replica import ReplicaTrainNode
+    trainer = config.trainer_class(model=config.model, train_dataset=config.train_dataset,
+                                   val_dataset=config.val_dataset, **config.kwargs)
+    for f in _FIELDS:
+        setattr(trainer, f, getattr(config, f))
+    trainer.rank = rank
+    trainer.world_size = procs
+    trainer._build_connection()
+    strategy = copy.deepcopy(trainer.strategy)
+    node = ReplicaTrainNode(trainer.model_orig, trainer.train_dataset, trainer.val_dataset, strategy, trainer.device,
+                            rank, trainer.num_nodes, K, num_epochs=trainer.num_epochs, max_steps=trainer.max_steps,
+                            batch_size=trainer.batch_size, minibatch_size=trainer.minibatch_size,
+                            val_size=trainer.val_size, val_interval=trainer.val_interval, shuffle=trainer.shuffle,
+                            autocast=trainer.autocast, **trainer.kwargs)
+    states = node.train()
+    trainer._process_cleanup()
+    for k, sd in enumerate(states):
+        result_queue.put((rank * K + k, OrderedDict((n, v.detach().cpu()) for n, v in sd.items())))
+
+
 def _average_model_states(model_states: Dict[int, OrderedDict]) -> Optional[OrderedDict]:
     """Mean over nodes of every state-dict entry; integer entries are averaged
     in float and cast back (trainer.py:95-119)."""
@@ -124,9 +147,17 @@ class Trainer:
                                 val_size=val_size, val_interval=val_interval, autocast=autocast,
                                 checkpoint_interval=checkpoint_interval, trainer_class=self.__class__,
                                 kwargs=self.kwargs)
+        from .replica import replica_layout
+        devs = devices if devices is not None else list(range(max(1, torch.cuda.device_count())))
+        layout = replica_layout(num_nodes, devs, self.kwargs.pop("replicas_per_process", "auto"), strategy)
+        config.kwargs = self.kwargs
         manager = mp.Manager()
         queue = manager.Queue()
-        mp.spawn(_worker, args=(config, queue), nprocs=num_nodes, start_method="spawn", join=True)
+        if layout is None:  # one process per simulated node (trainer.py:222-228)
+            mp.spawn(_worker, args=(config, queue), nprocs=num_nodes, start_method="spawn", join=True)
+        else:  # one process per GPU, K simulated nodes each on a [K, ld] replica arena
+            procs, K = layout
+            mp.spawn(_replica_worker, args=(config, procs, K, queue), nprocs=procs, start_method="spawn", join=True)
         states = {}
         for _ in range(num_nodes):
             r, sd = queue.get()
@@ -185,9 +216,10 @@ class LocalTrainer(Trainer):
             raise RuntimeError("LocalTrainer: no GPU visible (gym_amd has no CPU path)")
         if self.devices is None:
             self.devices = list(range(torch.cuda.device_count()))
+        world = getattr(self, "world_size", None) or self.num_nodes  # processes (< num_nodes with replicas)
         gpu = self.devices[self.rank % len(self.devices)]
         torch.cuda.set_device(gpu)
-        backend = select_backend(self.num_nodes, self.devices)
+        backend = select_backend(world, self.devices)
         kw = {"device_id": torch.device(f"cuda:{gpu}")} if backend == "nccl" else {}
-        dist.init_process_group(backend, rank=self.rank, world_size=self.num_nodes, **kw)
+        dist.init_process_group(backend, rank=self.rank, world_size=world, **kw)
         self.device = torch.device(f"cuda:{gpu}")

@@ -208,22 +208,25 @@ GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, int32_t nten
 GA_API int ga_sumsq_partials_count(void);
 
 /*
- * Gradient-norm clipping coefficient over a whole gradient arena of n elements:
- *   out[1] = ||grad||_2 (fp32 partial sums in a fixed order), and
- *   out[0] = min(1, max_norm / (out[1] + 1e-6)).
- * Both on the device (nothing synchronises); ga_adam_step applies out[0].
+ * Gradient-norm clipping coefficient per replica k < K of a gradient replica set
+ * (replica k: n elements at grad + k*ld):
+ *   out[2k+1] = ||grad_k||_2 (fp32 partial sums in a fixed order), and
+ *   out[2k]   = min(1, max_norm / (out[2k+1] + 1e-6)).
+ * `partials` holds K * ga_sumsq_partials_count() floats.  Device side only
+ * (nothing synchronises); ga_adam_step applies out[2k] to replica k.
  * Replaces: torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm) at
  * exogym/strategy/strategy.py:135-138, communicate_optimize_strategy.py:69-71,
  * diloco.py:52-56 (the per-tensor norms + stack + norm + per-tensor mul_).
  */
-GA_API int ga_grad_clip_coef(int dtype, const void* grad, int64_t n, float max_norm, float* partials,
-                             float* out, hipStream_t stream);
+GA_API int ga_grad_clip_coef(int dtype, const void* grad, int64_t K, int64_t ld, int64_t n, float max_norm,
+                             float* partials, float* out, hipStream_t stream);
 
 /*
- * One fused Adam/AdamW step over an fp32 arena (param, grad, exp_avg,
- * exp_avg_sq: n elements each, 16-byte aligned), in torch's op order
+ * One fused Adam/AdamW step over K replicas of an fp32 arena (param, grad,
+ * exp_avg, exp_avg_sq: [K, ld] sets, n elements per replica, 16-byte aligned),
+ * every replica with the same hyper-parameters, in torch's op order
  * (torch/optim/adam.py, _multi_tensor_adam):
- *   g = grad * clip_coef[0]   (and written back) if clip_coef != null and < 1
+ *   g = grad * clip_coef[2k]  (and written back) if clip_coef != null and < 1
  *   p *= wd_factor            (AdamW: 1 - lr*weight_decay, computed by the caller in double)
  *   g += l2_wd * p            (Adam with weight_decay)
  *   m = lerp(m, g, lerp_w)    (lerp_w = 1 - beta1)
@@ -233,9 +236,10 @@ GA_API int ga_grad_clip_coef(int dtype, const void* grad, int64_t n, float max_n
  * torch.optim.AdamW (exogym/strategy/strategy.py:140, diloco.py:59,
  * communicate_optimize_strategy.py:74; OptimSpec default optim.py:11).
  */
-GA_API int ga_adam_step(int dtype, void* param, void* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-                        float lerp_w, float beta2, float one_m_beta2, float eps, float wd_factor, float l2_wd,
-                        float step_size, float bc2_sqrt, const float* clip_coef, hipStream_t stream);
+GA_API int ga_adam_step(int dtype, void* param, void* grad, float* exp_avg, float* exp_avg_sq, int64_t K,
+                        int64_t ld, int64_t n, float lerp_w, float beta2, float one_m_beta2, float eps,
+                        float wd_factor, float l2_wd, float step_size, float bc2_sqrt, const float* clip_coef,
+                        hipStream_t stream);
 
 #ifdef __cplusplus
 }

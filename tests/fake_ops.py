@@ -131,24 +131,36 @@ def demo_decode(plan, gathered, param, grad, lr):
                 G[k, off:off + nel] = sgn
 
 
-def sumsq_partials(device):
-    return torch.zeros(1024, dtype=torch.float32, device=device)
+def sumsq_partials(device, K=1):
+    return torch.zeros(1024 * K, dtype=torch.float32, device=device)
 
 
 def grad_clip_coef(grad, n, max_norm, partials, out):
     from oracle import optim as ooptim
-    c, total = ooptim.clip_coef([_np(grad)[:n]], max_norm)
-    out[0] = c
-    out[1] = total
+    g2 = _2d(grad)
+    for k in range(g2.shape[0]):
+        c, total = ooptim.clip_coef([_np(g2[k])[:n]], max_norm)
+        out[2 * k] = c
+        out[2 * k + 1] = total
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size,
-              bc2_sqrt, clip_coef=None):
+              bc2_sqrt, clip_coef=None, n=None):
     """The fused step's arithmetic on CPU tensors (oracle/optim.py order)."""
+    P2, G2, M2, V2 = (_2d(t) for t in (param, grad, exp_avg, exp_avg_sq))
+    n = P2.shape[1] if n is None else int(n)
+    for k in range(P2.shape[0]):
+        c = None if clip_coef is None else float(clip_coef[2 * k])
+        _adam_one(P2[k, :n], G2[k, :n], M2[k, :n], V2[k, :n], lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd,
+                  step_size, bc2_sqrt, c)
+
+
+def _adam_one(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size,
+              bc2_sqrt, coef):
     f = np.float32
     p, g, m, v = _np(param).copy(), _np(grad).copy(), _np(exp_avg).copy(), _np(exp_avg_sq).copy()
-    if clip_coef is not None and float(clip_coef[0]) < 1.0:
-        g = (g * f(float(clip_coef[0]))).astype(f)
+    if coef is not None and coef < 1.0:
+        g = (g * f(coef)).astype(f)
         grad.copy_(torch.from_numpy(g))
     if wd_factor != 1.0:
         p = (p * f(wd_factor)).astype(f)
@@ -169,12 +181,13 @@ def install(monkeypatch_target_modules=None):
     let CPU models through the GPU check."""
     import gym_amd.engine as engine
     import gym_amd.fused_optim as fused_optim
+    import gym_amd.replica as replica
     import gym_amd.strategy.diloco as diloco
     import gym_amd.strategy.federated_averaging as fedavg
     import gym_amd.strategy.strategy as strategy
     import sys
     me = sys.modules[__name__]
-    for mod in (engine, diloco, fedavg, fused_optim):
+    for mod in (engine, diloco, fedavg, fused_optim, replica):
         mod.ops = me
     strategy.require_gpu = lambda device: None
     import gym_amd.strategy.demo_impl.demo as demo_mod

@@ -1,0 +1,47 @@
+"""Batched-replica node loop (gym_amd.replica) == the process-per-node
+strategies, on CPU with the oracle-backed kernel stand-ins (host logic: arena
+rows, engines over K local nodes, per-node clipping, fused optimizer over the
+replica set, gating); tests/test_gpu_replica.py runs the same with the kernels."""
+import pytest
+
+import replica_scenarios as R
+
+NAMES = ["simple", "diloco", "sparta", "fedavg", "demo"]
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    import fake_ops
+    import gym_amd.engine as engine
+    import gym_amd.fused_optim as fused_optim
+    import gym_amd.replica as replica
+    import gym_amd.strategy.demo_impl.demo as demo_mod
+    import gym_amd.strategy.diloco as diloco
+    import gym_amd.strategy.federated_averaging as fedavg
+    import gym_amd.strategy.strategy as strategy
+    for mod in (engine, diloco, fedavg, fused_optim, replica):
+        monkeypatch.setattr(mod, "ops", fake_ops)
+    monkeypatch.setattr(strategy, "require_gpu", lambda device: None)
+    monkeypatch.setattr(demo_mod, "_REQUIRE_GPU", False)
+    return fake_ops
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_replicas_match_process_per_node(tmp_path, fake, name):
+    proc = R.run_process_mode(name, 3, "cpu", True, str(tmp_path))
+    rep = R.run_replica_mode(name, 3, "cpu", True)
+    R.compare(proc, rep)
+
+
+def test_replica_layout_rules():
+    from gym_amd.replica import replica_layout
+    from gym_amd.strategy import SPARTAStrategy
+    s = R.make_strategy("simple")
+    assert replica_layout(4, [0, 1, 2, 3], "auto", s) is None          # one node per GPU
+    assert replica_layout(16, [0, 1, 2, 3], "auto", s) == (4, 4)       # 4 per GPU
+    assert replica_layout(6, [0, 1, 2, 3], "auto", s) is None          # not a multiple: gloo path
+    assert replica_layout(8, [0, 1], 4, s) == (2, 4)
+    assert replica_layout(8, [0, 1], 1, s) is None
+    assert replica_layout(8, [0], "auto", SPARTAStrategy(mask_source="torch")) is None
+    with pytest.raises(ValueError):
+        replica_layout(8, [0], 4, s)  # 2 processes on 1 GPU
