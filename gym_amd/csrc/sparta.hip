@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
                                                                  int64_t cap, int32_t* __restrict__ idx,
                                                                  T* __restrict__ vals, float divisor) {
     __shared__ int wave_tot[4];
-    __shared__ int32_t sel_list[kSpTile];
+    __shared__ uint16_t sel_list[kSpTile];  // tile-local positions (< 4096)
     __shared__ float gv[kGatherSlots];
     __shared__ float gavg[kSpBlock];
     const int64_t tile0 = (int64_t)blockIdx.x * kSpTile;
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
         const int j = __ffs(bits) - 1;
         bits &= bits - 1;
         const int32_t i = (int32_t)(threadIdx.x * kSpPerThread + j);
-        sel_list[local] = i;
+        sel_list[local] = (uint16_t)i;
         const int64_t pos = out0 + local;
         if (idx && pos < cap) idx[pos] = (int32_t)(tile0 + i);
         ++local;
@@ -200,9 +200,25 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
             // replica-major lanes: consecutive lanes read consecutive selected
             // elements of ONE replica (same 16 KB tile -> few DRAM pages)
             const int Ki = (int)K;
-            for (int f = threadIdx.x; f < ce * Ki; f += kSpBlock) {
-                const int k = f / ce, e = f - k * ce;
-                gv[e * Ki + k] = Elem<T>::load(src + (int64_t)k * ld + tile0 + sel_list[c0 + e]);
+            // every lane's loads of the pass issued back to back (one HBM latency
+            // per pass instead of one per load), then staged into LDS
+            constexpr int kLoads = kGatherSlots / kSpBlock;
+            float v[kLoads];
+#pragma unroll
+            for (int u = 0; u < kLoads; ++u) {
+                const int f = threadIdx.x + u * kSpBlock;
+                if (f < ce * Ki) {
+                    const int k = f / ce, e = f - k * ce;
+                    v[u] = Elem<T>::load(src + (int64_t)k * ld + tile0 + sel_list[c0 + e]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kLoads; ++u) {
+                const int f = threadIdx.x + u * kSpBlock;
+                if (f < ce * Ki) {
+                    const int k = f / ce, e = f - k * ce;
+                    gv[e * Ki + k] = v[u];
+                }
             }
             __syncthreads();
             if (threadIdx.x < ce) {
