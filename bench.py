@@ -225,7 +225,7 @@ def bench_sparta(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
     return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
             "K_local": K, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1),
             "path": "fused select+gather+average+write-back" if coll.world == 1 else
-                    "select+gather, RCCL all-reduce of packed values, scatter"}
+                    f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter"}
 
 
 def bench_simple(args, coll, dev, K=8, model="gpt2-char"):
