@@ -258,8 +258,16 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
         R, C, n1, n2 = codec_view(s, 64)
         flops_one += 2 * (R // n1) * (C // n2) * 2 * 64 ** 3  # two zero-padded 64^3 products per transform
     enc_ms, dec_ms = te.mean_ms(), td.mean_ms()
+    # the decode of 8 gathered payloads (what every GPU runs at 8 nodes), here from
+    # 8 copies of this node's payload: scatter-mean + the dense symmetric inverse
+    gathered8 = codec.payload[0:1].expand(8, -1).contiguous()
+    t8 = KernelTimer()
+    dec8 = t8.wrap(lambda: ops.demo_decode(plan, gathered8, P, G, 1e-3))
+    t8.on = True
+    timed_loop(dec8, args.steps, args.warmup, coll)
+    dec8_ms = t8.mean_ms()
     return {"ms_per_step": round(t * 1e3, 4), "model": model, "nodes": coll.world,
-            "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+            "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4), "decode_8src_ms": round(dec8_ms, 4),
             "encode_TFLOPs": round(2 * flops_one / (enc_ms * 1e-3) / 1e12, 2),
             "decode_TFLOPs": round(flops_one / (dec_ms * 1e-3) / 1e12, 2),
             "mfma_f32_peak_TFLOPs": MFMA_F32_TFLOPS, "payload_entries": plan.M,

@@ -177,6 +177,45 @@ __device__ __forceinline__ f32x16 mm_sym2(const float* T, const float* FT, int t
     return acc;
 }
 
+// Inverse transforms with the same symmetry (decode, several sources):
+// U = S . F2^T with U[b][j] = Ue + Uo, U[b][63-j] = Ue - Uo (j < 32), where
+// Ue/Uo sum over the even/odd columns d of S.  Wave (qr, par) computes rows
+// 32qr.. of U' = [Ue | Uo] (K = 32), stored back as that quadrant.
+__device__ __forceinline__ f32x16 mm_isym1(const float* S, const float* FT, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    const int qr = w >> 1, par = w & 1, h = lane >> 5, l = lane & 31;
+    const float* A = S + (32 * qr + l) * kLd + par;
+    const float* Bm = FT + l * kLd + par;
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int k = 2 * (2 * s + h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[k], Bm[k], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+// g = F1 . U with g[i] = ge + go, g[63-i] = ge - go (i < 32), ge/go summing over
+// the even/odd rows b of U, U read from U' (mm_isym1).  Wave (par, qc) computes
+// rows i < 32 of ge (par 0) / go (par 1) for natural columns 32qc.., stored at
+// tile rows 32*par + i: the [ge ; go] layout the split read combines.
+__device__ __forceinline__ f32x16 mm_isym2(const float* U, const float* FT, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    const int par = w >> 1, qc = w & 1, h = lane >> 5, l = lane & 31;
+    const float* A = FT + l * kLd + par;
+    // U[b][32qc + l]: qc 0 -> U'[b][l] + U'[b][32 + l]; qc 1 -> U'[b][31 - l] - U'[b][63 - l]
+    const float* U0 = U + (qc ? 31 - l : l);
+    const float sg = qc ? -1.f : 1.f;
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int k = 2 * (2 * s + h);  // b = k + par
+        const float* row = U0 + (k + par) * kLd;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A[k], fmaf(sg, row[32], row[0]), acc, 0, 0, 0);
+    }
+    return acc;
+}
+
 // Natural (row, column) of this lane's accumulators and the tile position of a
 // natural coefficient, for the plain and the permuted (symmetric) layouts.
 struct Perm {
@@ -878,6 +917,8 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
         }
         const int64_t eoff = td.payload_off + (int64_t)c * nk;
         f32x16 acc;
+        // the dense (several-source) inverse uses the DCT symmetry for 64-point bases
+        const bool dsym = nsrc > 1 && n2 == 64 && (n1 == 64 || n1 == 1);  // uniform
         const int next = chunk + (int)gridDim.x;
         const bool more = next < nchunks;
         int tixn = tix;
@@ -936,12 +977,14 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
             }
             LDS_BARRIER();
             // g = B1^T . S . B2 = F1 . S . F2^T on the matrix cores, in place in S
-            acc = mm64<TILE_ROW, TILE_COL>(S, FT, tid);  // U = S . F2^T
+            // (half the MFMAs for 64-point bases: mm_isym1 / mm_isym2)
+            acc = dsym ? mm_isym1(S, FT, tid) : mm64<TILE_ROW, TILE_COL>(S, FT, tid);  // U = S . F2^T
             LDS_BARRIER();
             store_acc(S, acc, tid);
             LDS_BARRIER();
             if (n1 > 1) {
-                if (td.basis1 == td.basis2) acc = mm64<TILE_ROW, TILE_ROW>(FT, S, tid);  // F1 . U
+                if (dsym) acc = mm_isym2(S, FT, tid);  // F1 . U
+                else if (td.basis1 == td.basis2) acc = mm64<TILE_ROW, TILE_ROW>(FT, S, tid);
                 else acc = mm64<GTAB_COL, TILE_ROW>(B + (int64_t)td.basis1 * 4096, S, tid);  // F1[i][k] = B1[k][i]
                 LDS_BARRIER();
             }
@@ -958,7 +1001,13 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
             float sg[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float gv = S[io.row(i) * kLd + io.col0() + e];
+                const int rr = io.row(i), cc = io.col0() + e;
+                float gv;
+                if (!dsym) gv = S[rr * kLd + cc];
+                else if (n1 == 1) gv = cc < 32 ? S[rr * kLd + cc] + S[rr * kLd + 32 + cc]  // [Ue | Uo] of row 0
+                                               : S[rr * kLd + 63 - cc] - S[rr * kLd + 95 - cc];
+                else if (i < 2) gv = S[rr * kLd + cc] + S[(32 + rr) * kLd + cc];  // [ge ; go], rows < 32
+                else gv = S[(63 - rr) * kLd + cc] - S[(95 - rr) * kLd + cc];
                 sg[e] = (float)((gv > 0.f) - (gv < 0.f));
             }
             if (io.live(i)) {
