@@ -222,8 +222,13 @@ def bench_sparta(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
     ops.sparta_select(rs.data, layout.n, eng.cap, eng.idx, eng.vals, eng.count, eng.work, seed=42, iteration=0, p=p)
     M = int(eng.count[0].item())
     alg = 2 * 4 * K * M + (8 * M if coll.world > 1 else 0)  # K-replica gather + write-back (+ idx/vals list)
+    # what HBM must move at its access granularity: each selected (element, replica)
+    # is a random 4-B word -> one 64-B read sector + one 32-B write sector
+    # (rocprofv3 FETCH_SIZE/WRITE_SIZE of this kernel: 1.18 GB + 0.61 GB per step)
+    sect = (64 + 32) * K * M
     return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
             "K_local": K, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1),
+            "sector_bytes": sect, "sector_GBps": round(sect / t / 1e9, 1),
             "path": "fused select+gather+average+write-back" if coll.world == 1 else
                     f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter"}
 

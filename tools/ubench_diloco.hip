@@ -144,6 +144,32 @@ __global__ __launch_bounds__(256) void v_chunk(const float* src, long ld, long n
     }
 }
 
+// persistent contiguous ranges: workgroup b streams vectors [b*per, (b+1)*per)
+template <int K, bool NTL>
+__global__ __launch_bounds__(256) void v_persist(const float* src, long ld, long n, float* master, float* mom, OP op,
+                                                 float* dst) {
+    const long nv = n >> 2;
+    const long per = (nv + gridDim.x - 1) / gridDim.x;
+    const long lo = (long)blockIdx.x * per;
+    const long hi = lo + per < nv ? lo + per : nv;
+    for (long v = lo + threadIdx.x; v < hi; v += 256) {
+        float4 x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[k] = ld4<NTL>(reinterpret_cast<const float4*>(src + k * ld) + v);
+        float4 m = reinterpret_cast<const float4*>(master)[v], b = reinterpret_cast<const float4*>(mom)[v];
+        float a[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < K; ++k) { a[0] += x[k].x; a[1] += x[k].y; a[2] += x[k].z; a[3] += x[k].w; }
+        float4 o;
+        o.x = upd(a[0], m.x, b.x, op); o.y = upd(a[1], m.y, b.y, op);
+        o.z = upd(a[2], m.z, b.z, op); o.w = upd(a[3], m.w, b.w, op);
+        reinterpret_cast<float4*>(master)[v] = m;
+        reinterpret_cast<float4*>(mom)[v] = b;
+#pragma unroll
+        for (int k = 0; k < K; ++k) reinterpret_cast<float4*>(dst + k * ld)[v] = o;
+    }
+}
+
 __global__ void copy4(const float4* a, float4* b, long nv) {
     long stride = (long)gridDim.x * blockDim.x;
     for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) b[v] = a[v];
@@ -202,6 +228,17 @@ int main() {
         float ms = time_ms([&] { v_chunk<K, CH, U, NTS><<<g, 256>>>(src, ld, n, master, mom, op, src); }, reps); \
         printf("chunk CH=%d U=%d nts=%d grid %6d: %.3f ms  %.0f GB/s\n", CH, U, NTS, g, ms, bytes / ms / 1e6); \
     }
+#define RUNP(G, NTL)                                                                                     \
+    {                                                                                                     \
+        float ms = time_ms([&] { v_persist<K, NTL><<<G, 256>>>(src, ld, n, master, mom, op, src); }, reps);  \
+        printf("persist G=%d ntl=%d: %.3f ms  %.0f GB/s\n", G, NTL, ms, bytes / ms / 1e6);                 \
+    }
+    RUNP(512, false)
+    RUNP(1024, false)
+    RUNP(2048, false)
+    RUNP(4096, false)
+    RUNP(1024, true)
+    RUNP(2048, true)
     RUNC(1024, 1, false)
     RUNC(1024, 1, false)
     RUNC(512, 1, false)
