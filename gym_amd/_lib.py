@@ -35,6 +35,11 @@ class DemoTensor(ctypes.Structure):
     ]
 
 
+class DemoRowGroup(ctypes.Structure):
+    """Mirror of `ga_demo_rowgroup` (include/gym_amd.h)."""
+    _fields_ = [("offset", c_i64), ("payload_off", c_i64), ("rows", c_i32), ("k", c_i32)]
+
+
 # name -> (restype, argtypes); kept in the order of include/gym_amd.h
 SIGNATURES = {
     "ga_abi_version": (c_i32, []),
@@ -52,6 +57,8 @@ SIGNATURES = {
     "ga_demo_tensor_bytes": (c_i32, []),
     "ga_demo_encode": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32,
                                c_f32, c_p, c_i64, c_i64, c_p]),
+    "ga_demo_encode_sym": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64,
+                                   c_f32, c_f32, c_f32, c_p, c_i64, c_i64, c_p]),
     "ga_demo_decode": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64,
                                c_i64, c_f32, c_p]),
     "ga_sumsq_partials_count": (c_i32, []),

@@ -1,0 +1,785 @@
+// DeMo encode, register-resident wave-per-chunk form (ga_demo_encode_sym).
+//
+// Same contract and arithmetic as ga_demo_encode (demo.hip; demo.py:142-209),
+// for plans whose chunks are all 64x64 or 1x64 with k <= 64 -- DeMo's
+// compression_chunk = 64 on GPT-2-shaped models.  One wavefront owns a whole
+// 64x64 chunk and keeps it in registers from the load to the delta store: no
+// workgroup barrier in the chunk loop, and LDS only for the shared half basis
+// and the top-k candidate list.  The 8 waves of a CU (2 per SIMD) interleave
+// freely, one wave's MFMA chain running while another waits on its loads.
+//
+// Lane (l, h) = (lane & 31, lane >> 5) holds data rows l and 63 - l, columns
+// S_h (eight 4-column blocks BL_h: h = 0 -> blocks 0-3, 12-15; h = 1 -> 4-11),
+// a set closed under j -> 63 - j.  With the DCT symmetry
+// F[63 - i][k] = (-1)^k F[i][k] every product is a 32-deep MFMA chain whose
+// register operand is already in the right lane:
+//   T  = X . F2   per row pair: A = x[j] +- x[63 - j] (own registers),
+//                 B = F[j][2d' + qc] (LDS)               4 x 16 MFMAs
+//   Y  = F1^T . T: B = T[i] +- T[63 - i] (own accumulators; rows l and 63 - l
+//                 sit in the same register of the same lane), A = F[i][2b' + p]
+//                                                        4 x 16 MFMAs
+//   R^T = sum_e (v_e F[c][d_e]) (x) F[i][b_e] per parity of b_e, so that R
+//                 lands in the load layout (column c = pi(m) of accumulator row
+//                 m is the lane's own column); rows 63 - l by the symmetry
+//                                                        ~k + 2 MFMAs
+// 1x64 chunks (vectors) are processed 64 at a time (a "row group", rows =
+// consecutive chunks): the same row product, then a per-lane exact top-k over
+// the lane's own row through one LDS tile, and the residual as a dense
+// R^T = F . Ymask^T product.
+//
+// Top-k (demo.py:315-328) is exact with ties to the lowest index; a chunk's
+// entries are emitted in ascending coefficient index, as ga_demo_encode.
+#include "ga_common.h"
+
+namespace ga {
+namespace dw {
+
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kLd = 65;     // LDS row stride (basis, row-group tile)
+constexpr int kCand = 128;  // fast-path candidate capacity
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#ifdef GA_DEMO_STAMPS
+extern __device__ unsigned long long* g_demo_stamps_w;
+#define DW_PH_DECL unsigned long long ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_last = __builtin_amdgcn_s_memtime()
+#define DW_PH(i)                                                    \
+    do {                                                            \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ph_acc[i] += t_ - ph_last;                                  \
+        ph_last = t_;                                               \
+    } while (0)
+#define DW_CNT(i) (ph_acc[i] += 1)
+#define DW_PH_FLUSH()                                                                                       \
+    do {                                                                                                    \
+        if ((threadIdx.x & 63) == 0) {                                                                      \
+            unsigned long long* row_ = g_demo_stamps_w + ((size_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 16; \
+            for (int i_ = 0; i_ < 10; ++i_) row_[i_] = ph_acc[i_];                                          \
+        }                                                                                                   \
+    } while (0)
+#else
+#define DW_PH_DECL do {} while (0)
+#define DW_PH(i) do {} while (0)
+#define DW_CNT(i) do {} while (0)
+#define DW_PH_FLUSH() do {} while (0)
+#endif
+
+// Lanes of one wave hand data to each other through LDS: keep the compiler
+// from moving this lane's LDS accesses across the hand-off (the hardware runs
+// a wave's LDS operations in order).
+#define WAVE_LDS_SYNC() asm volatile("" ::: "memory")
+
+__device__ __forceinline__ int lane_id() {
+    int t = (int)threadIdx.x;
+    asm volatile("" : "+v"(t));  // not hoisted out of the chunk loop (see demo.hip opaque_tid)
+    return t & 63;
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+    f32x16 a;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[r] = 0.f;
+    return a;
+}
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// accumulator register r of lane half h: row (r & 3) + 8 (r >> 2) + 4 h of the 32x32 block
+__device__ __forceinline__ constexpr int rowmap(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// column block q (0..7) of lane half h
+__device__ __forceinline__ int blk(int h, int q) { return h ? 4 + q : (q < 4 ? q : 8 + q); }
+
+// data column of residual accumulator half H, accumulator row m (the lane's own column, see header)
+__device__ __forceinline__ int pi_col(int H, int m) { return 4 * blk((m >> 2) & 1, 4 * H + (m >> 3)) + (m & 3); }
+
+// F[i][d] (0 <= i < 64) from the half table H = F[0..31][:]
+__device__ __forceinline__ float basis64(const float* Hb, int i, int d) {
+    const float v = Hb[(i < 32 ? i : 63 - i) * kLd + d];
+    return (i >= 32 && (d & 1)) ? -v : v;
+}
+
+__device__ __forceinline__ uint32_t keyv(float v) { return (__float_as_uint(v) & 0x7fffffffu) + 1u; }
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(v, d, 64);
+        if (lane >= d) v += y;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, j);
+}
+
+struct WaveLDS {
+    uint32_t lst[2 * (kCand + 64)];  // candidates (pos, bits); slots kCand + lane: discard
+    uint32_t bm[128];                // 4096-bit position bitmap
+    uint32_t sm[4];                  // 128-bit rank-space selection mask
+    float tile[64 * kLd];            // row groups: T, then the masked coefficients
+};
+
+// ---- operands in registers --------------------------------------------------
+// x[s][q][e]: row l (s = 0) or 63 - l (s = 1), column 4 blk(h, q) + e
+// lane offset of x[s][q][0] from the chunk's (0, 0) element (32-bit: a chunk spans < 2^31 elements)
+__device__ __forceinline__ int lane_off(int s, int q, int l, int h, int stride) {
+    return (s ? 63 - l : l) * stride + 4 * blk(h, q);
+}
+
+// pb: the chunk's (0, 0) element (wave-uniform pointer; the lane part is a 32-bit offset)
+template <typename T>
+__device__ __forceinline__ void load_rows(const T* pb, int stride, int l, int h, bool vec, int nrows,
+                                          float (&o)[2][8][4]) {
+    if (vec && nrows == 64) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(pb + lane_off(s, q, l, h, stride)),
+                                o[s][q]);
+        return;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const bool live = (s ? 63 - l : l) < nrows;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const T* a = pb + lane_off(s, q, l, h, stride);
+            if (live && vec) {
+                Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(a), o[s][q]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[s][q][e] = live ? Elem<T>::load(a + e) : 0.f;
+            }
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_rows(T* pb, int stride, int l, int h, bool vec, int nrows,
+                                           const float (&o)[2][8][4]) {
+    if (vec && nrows == 64) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                *reinterpret_cast<typename Vec4<T>::type*>(pb + lane_off(s, q, l, h, stride)) = Vec4<T>::pack(o[s][q]);
+        return;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        if ((s ? 63 - l : l) >= nrows) continue;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            T* a = pb + lane_off(s, q, l, h, stride);
+            if (vec) {
+                *reinterpret_cast<typename Vec4<T>::type*>(a) = Vec4<T>::pack(o[s][q]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Elem<T>::store(a + e, o[s][q][e]);
+            }
+        }
+    }
+}
+
+// x = decay*delta + lr*grad (+ p *= wd_factor): demo.py:159-167, same rounding as ga_demo_encode
+template <typename T>
+__device__ __forceinline__ void error_feedback(T* param, const T* grad, const T* delta, int stride, int l, int h,
+                                               bool vec, int nrows, float lr, float decay, float wd_factor,
+                                               float (&x)[2][8][4]) {
+    if (wd_factor != 1.f) {  // its own pass: p is read and written before d, g are loaded
+        load_rows(param, stride, l, h, vec, nrows, x);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[s][q][e] *= wd_factor;
+        store_rows(param, stride, l, h, vec, nrows, x);
+    }
+    float g[2][8][4];
+    load_rows(delta, stride, l, h, vec, nrows, x);
+    load_rows(grad, stride, l, h, vec, nrows, g);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                x[s][q][e] = fmaf(lr, g[s][q][e], decay != 1.f ? x[s][q][e] * decay : x[s][q][e]);
+}
+
+// T[s][qc] = rows of X (s = 0: rows l, 1: rows 63 - l) times F2, even (qc = 0) or
+// odd (qc = 1) frequencies d = 2 col + qc; K index of step t, half h: column 16h + t
+__device__ __forceinline__ void row_product(const float (&x)[2][8][4], const float* Hb, int l, int h,
+                                            f32x16 (&T)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int qc = 0; qc < 2; ++qc) {
+            f32x16 acc = zero16();
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int q = t >> 2, e = t & 3;
+                const float u = x[s][q][e], w = x[s][7 - q][3 - e];
+                const float a = qc ? u - w : u + w;
+                acc = mfma(a, Hb[(16 * h + t) * kLd + 2 * l + qc], acc);
+            }
+            T[s][qc] = acc;
+        }
+    }
+}
+
+// ---- 64x64 chunk ------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* param, const T* grad, T* delta,
+                                        int32_t* out_idx, float* out_val, float lr, float decay, float wd_factor,
+                                        int ptr_vec, const float* Hb, WaveLDS& W
+#ifdef GA_DEMO_STAMPS
+                                        , unsigned long long (&ph_acc)[10], unsigned long long& ph_last
+#endif
+) {
+    const int k = td.k;
+    const int cy = c / td.gx, cx = c - cy * td.gx;
+    const int64_t base = td.offset + (int64_t)cy * 64 * td.cols + (int64_t)cx * 64;
+    param += base;
+    grad += base;
+    delta += base;
+    const bool vec = ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0);
+    float4* park = reinterpret_cast<float4*>(W.tile);  // x while the products and the top-k run
+    float x[2][8][4];
+    {
+        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+        error_feedback(param, grad, delta, td.cols, l, h, vec, 64, lr, decay, wd_factor, x);
+    }
+    DW_PH(0);
+    f32x16 Y[2][2];  // [parity of b][qc]
+    {
+        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+        f32x16 Tm[2][2];
+        row_product(x, Hb, l, h, Tm);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                park[(8 * s + q) * 64 + lane] = make_float4(x[s][q][0], x[s][q][1], x[s][q][2], x[s][q][3]);
+        DW_PH(1);
+#pragma unroll
+        for (int qc = 0; qc < 2; ++qc) {
+#pragma unroll
+            for (int par = 0; par < 2; ++par) {
+                f32x16 acc = zero16();
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const float u = Tm[0][qc][t], w = Tm[1][qc][t];
+                    acc = mfma(Hb[rowmap(t, h) * kLd + 2 * l + par], par ? u - w : u + w, acc);
+                }
+                Y[par][qc] = acc;
+            }
+        }
+    }
+    DW_PH(2);
+    // ---- top-k: register t = 32 par + 16 qc + r holds coefficient
+    //      b = 2 rowmap(r, h) + par, d = 2 l + qc
+    const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+    auto posof = [&](int par, int qc, int r) -> uint32_t {
+        return (uint32_t)((2 * rowmap(r, h) + par) * 64 + 2 * l + qc);
+    };
+    // |v| >= f(T) <=> keyv(v) >= T with f(T) = as_float(T - 1) (non-NaN v; abs is a free operand modifier)
+    float mymaxf = 0.f;
+#pragma unroll
+    for (int par = 0; par < 2; ++par)
+#pragma unroll
+        for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mymaxf = fmaxf(mymaxf, fabsf(Y[par][qc][r]));
+    const uint32_t mymax = keyv(mymaxf);
+    uint32_t T0 = 0;
+#pragma unroll
+    for (int bit = 30; bit >= 19; --bit) {
+        const uint32_t cnd = T0 | (1u << bit);
+        if (__popcll(__ballot(mymax >= cnd)) >= k) T0 = cnd;
+    }
+    if (T0 == 0u) T0 = 1u;
+    const float T0f = __uint_as_float(T0 - 1u);
+    int mine = 0;
+#pragma unroll
+    for (int par = 0; par < 2; ++par)
+#pragma unroll
+        for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mine += fabsf(Y[par][qc][r]) >= T0f ? 1 : 0;
+    const int incl = wave_incl_scan(mine, lane);
+    const int C = __builtin_amdgcn_readlane(incl, 63);
+    W.bm[2 * lane] = 0u;
+    W.bm[2 * lane + 1] = 0u;
+    if (C <= kCand) {
+        // compact the candidates: (pos, bits) at the lane's next slot, others to its discard slot
+        int at = incl - mine;
+        uint2* L2 = reinterpret_cast<uint2*>(W.lst);
+        float T0c = T0f;  // an opaque copy: the 64 compares are redone here, not kept as 64 lane masks
+        asm volatile("" : "+v"(T0c));
+#pragma unroll
+        for (int par = 0; par < 2; ++par)
+#pragma unroll
+            for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float v = Y[par][qc][r];
+                    const bool cnd = fabsf(v) >= T0c;
+                    L2[cnd ? at : kCand + lane] = make_uint2(posof(par, qc, r), __float_as_uint(v));
+                    at += cnd ? 1 : 0;
+                }
+        WAVE_LDS_SYNC();
+        uint32_t pos[2], bits[2], key[2];
+        bool ok[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int g = e * 64 + lane;
+            ok[e] = g < C;
+            const uint2 pb = L2[ok[e] ? g : kCand + lane];
+            pos[e] = ok[e] ? pb.x : 0u;
+            bits[e] = pb.y;
+            key[e] = ok[e] ? keyv(__uint_as_float(pb.y)) : 0u;
+            if (ok[e]) atomicOr(&W.bm[pos[e] >> 5], 1u << (pos[e] & 31));
+        }
+        WAVE_LDS_SYNC();
+        // rank of a candidate = candidates at lower positions (bitmap prefix counts)
+        const uint32_t w0 = W.bm[2 * lane], w1 = W.bm[2 * lane + 1];
+        const int cnt = __popc(w0) + __popc(w1);
+        const int pre = wave_incl_scan(cnt, lane) - cnt;
+        int rank[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int Lw = (int)(pos[e] >> 6);  // every lane takes part in the shuffles
+            const uint64_t pair = ((uint64_t)(uint32_t)__shfl((int)w1, Lw, 64) << 32) |
+                                  (uint32_t)__shfl((int)w0, Lw, 64);
+            const int preL = __shfl(pre, Lw, 64);
+            rank[e] = ok[e] ? preL + __popcll(pair & ((1ull << (pos[e] & 63)) - 1ull)) : 0x7fff;
+        }
+        // exact k-th key among the candidates
+        uint32_t thr = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t cnd = thr | (1u << bit);
+            if (__popcll(__ballot(key[0] >= cnd)) + __popcll(__ballot(key[1] >= cnd)) >= k) thr = cnd;
+        }
+        const int need = k - __popcll(__ballot(key[0] > thr)) - __popcll(__ballot(key[1] > thr));
+        const uint64_t q0 = __ballot(key[0] == thr), q1 = __ballot(key[1] == thr);
+        bool sel[2];
+        if (__popcll(q0) + __popcll(q1) == need) {
+            sel[0] = key[0] >= thr;
+            sel[1] = key[1] >= thr;
+        } else {  // ties at the k-th key: the lowest positions (ranks) win
+            int tr[2] = {0, 0};
+            for (uint64_t m = q0; m; m &= m - 1) {
+                const int rj = __builtin_amdgcn_readlane(rank[0], __builtin_ctzll(m));
+                tr[0] += rj < rank[0];
+                tr[1] += rj < rank[1];
+            }
+            for (uint64_t m = q1; m; m &= m - 1) {
+                const int rj = __builtin_amdgcn_readlane(rank[1], __builtin_ctzll(m));
+                tr[0] += rj < rank[0];
+                tr[1] += rj < rank[1];
+            }
+            sel[0] = key[0] > thr || (key[0] == thr && tr[0] < need);
+            sel[1] = key[1] > thr || (key[1] == thr && tr[1] < need);
+        }
+        if (lane < 4) W.sm[lane] = 0u;
+        WAVE_LDS_SYNC();
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (sel[e]) atomicOr(&W.sm[rank[e] >> 5], 1u << (rank[e] & 31));
+        WAVE_LDS_SYNC();
+        const uint64_t m0 = ((uint64_t)W.sm[1] << 32) | W.sm[0], m1 = ((uint64_t)W.sm[3] << 32) | W.sm[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            if (sel[e]) {
+                const int r = rank[e];
+                const int slot = r < 64 ? __popcll(m0 & ((1ull << r) - 1ull))
+                                        : __popcll(m0) + __popcll(m1 & ((1ull << (r - 64)) - 1ull));
+                W.lst[2 * slot] = pos[e];  // slots < k <= 64 <= the candidates' own range
+                W.lst[2 * slot + 1] = bits[e];
+                out_idx[slot] = (int32_t)pos[e];
+                out_val[slot] = __uint_as_float(bits[e]);
+            }
+        }
+        WAVE_LDS_SYNC();
+    } else {
+        // more than kCand keys >= T0 (flat spectra, all-zero chunks): exact k-th
+        // key over all 4096 keys, ties to the lowest positions, slots in position order
+        DW_CNT(8);
+        uint32_t thr = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t cnd = thr | (1u << bit);
+            int cl = 0;
+#pragma unroll
+            for (int par = 0; par < 2; ++par)
+#pragma unroll
+                for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) cl += fabsf(Y[par][qc][r]) >= __uint_as_float(cnd - 1u) ? 1 : 0;
+            if (wave_sum(cl) >= k) thr = cnd;
+        }
+        int gl = 0;
+#pragma unroll
+        for (int par = 0; par < 2; ++par)
+#pragma unroll
+            for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t kv = keyv(Y[par][qc][r]);
+                    gl += kv > thr ? 1 : 0;
+                    if (kv == thr) {
+                        const uint32_t p = posof(par, qc, r);
+                        atomicOr(&W.bm[p >> 5], 1u << (p & 31));
+                    }
+                }
+        const int need = k - wave_sum(gl);
+        WAVE_LDS_SYNC();
+        uint32_t w0 = W.bm[2 * lane], w1 = W.bm[2 * lane + 1];
+        int cnt = __popc(w0) + __popc(w1);
+        int pre = wave_incl_scan(cnt, lane) - cnt;
+        WAVE_LDS_SYNC();
+        W.bm[2 * lane] = 0u;  // becomes the selection bitmap
+        W.bm[2 * lane + 1] = 0u;
+        WAVE_LDS_SYNC();
+        // a tied coefficient's tie rank = tied positions below it
+#pragma unroll
+        for (int par = 0; par < 2; ++par)
+#pragma unroll
+            for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t kv = keyv(Y[par][qc][r]);
+                    const uint32_t p = posof(par, qc, r);
+                    const int Lw = (int)(p >> 6);
+                    const uint64_t pair = ((uint64_t)(uint32_t)__shfl((int)w1, Lw, 64) << 32) |
+                                          (uint32_t)__shfl((int)w0, Lw, 64);
+                    const int tr = __shfl(pre, Lw, 64) + __popcll(pair & ((1ull << (p & 63)) - 1ull));
+                    if (kv > thr || (kv == thr && tr < need)) atomicOr(&W.bm[p >> 5], 1u << (p & 31));
+                }
+        WAVE_LDS_SYNC();
+        w0 = W.bm[2 * lane];
+        w1 = W.bm[2 * lane + 1];
+        cnt = __popc(w0) + __popc(w1);
+        pre = wave_incl_scan(cnt, lane) - cnt;
+#pragma unroll
+        for (int par = 0; par < 2; ++par)
+#pragma unroll
+            for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const uint32_t p = posof(par, qc, r);
+                    const int Lw = (int)(p >> 6);
+                    const uint64_t pair = ((uint64_t)(uint32_t)__shfl((int)w1, Lw, 64) << 32) |
+                                          (uint32_t)__shfl((int)w0, Lw, 64);
+                    const int preL = __shfl(pre, Lw, 64);
+                    if ((pair >> (p & 63)) & 1ull) {
+                        const int slot = preL + __popcll(pair & ((1ull << (p & 63)) - 1ull));
+                        const float v = Y[par][qc][r];
+                        W.lst[2 * slot] = p;
+                        W.lst[2 * slot + 1] = __float_as_uint(v);
+                        out_idx[slot] = (int32_t)p;
+                        out_val[slot] = v;
+                    }
+                }
+        WAVE_LDS_SYNC();
+    }
+    DW_PH(3);
+    // ---- residual (demo.py:174-180) in the load layout: R^T per parity of b
+    const uint32_t epos = lane < k ? W.lst[2 * lane] : 0u;
+    const uint32_t ebits = lane < k ? W.lst[2 * lane + 1] : 0u;
+    f32x16 R[2][2];  // [parity][column half H]
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        R[par][0] = zero16();
+        R[par][1] = zero16();
+        uint64_t mk = __ballot(lane < k && (int)((epos >> 6) & 1u) == par);
+        const int c0 = pi_col(0, l), c1 = pi_col(1, l);
+        while (mk) {
+            const int j0 = __builtin_ctzll(mk);
+            mk &= mk - 1;
+            uint32_t p1 = 0u, v1 = 0u;
+            const uint32_t p0 = rdl(epos, j0), v0 = rdl(ebits, j0);
+            if (mk) {
+                const int j1 = __builtin_ctzll(mk);
+                mk &= mk - 1;
+                p1 = rdl(epos, j1);
+                v1 = rdl(ebits, j1);
+            }
+            const uint32_t pe = h ? p1 : p0;
+            const float ve = __uint_as_float(h ? v1 : v0);
+            const int bq = (int)(pe >> 6), dq = (int)(pe & 63);
+            const float bop = Hb[l * kLd + bq];  // F[l][b_e]
+            R[par][0] = mfma(ve * basis64(Hb, c0, dq), bop, R[par][0]);
+            R[par][1] = mfma(ve * basis64(Hb, c1, dq), bop, R[par][1]);
+        }
+    }
+    DW_PH(4);
+    // delta = x - R: row l gets Re + Ro, row 63 - l gets Re - Ro
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float4 v = park[(8 * s + q) * 64 + lane];
+            x[s][q][0] = v.x;
+            x[s][q][1] = v.y;
+            x[s][q][2] = v.z;
+            x[s][q][3] = v.w;
+        }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int Hh = q >> 2, r = 4 * (q & 3) + e;
+            const float re = R[0][Hh][r], ro = R[1][Hh][r];
+            x[0][q][e] -= re + ro;
+            x[1][q][e] -= re - ro;
+        }
+    store_rows(delta, td.cols, l, h, vec, 64, x);
+    WAVE_LDS_SYNC();
+    DW_PH(5);
+}
+
+// ---- row group: up to 64 consecutive 1x64 chunks (F1 = [1]) ---------------
+template <typename T>
+__device__ __forceinline__ void rowgroup(const ga_demo_rowgroup& rg, T* param, const T* grad, T* delta,
+                                         int32_t* pay_idx, float* pay_val, float lr, float decay,
+                                         float wd_factor, int ptr_vec, const float* Hb, WaveLDS& W
+#ifdef GA_DEMO_STAMPS
+                                         , unsigned long long (&ph_acc)[10], unsigned long long& ph_last
+#endif
+) {
+    const int rows = rg.rows, k = rg.k;
+    const bool vec = ptr_vec && (rg.offset % 4 == 0);
+    param += rg.offset;
+    grad += rg.offset;
+    delta += rg.offset;
+    float x[2][8][4];
+    {
+        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+        error_feedback(param, grad, delta, 64, l, h, vec, rows, lr, decay, wd_factor, x);
+    }
+    DW_PH(6);
+    {
+        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+        f32x16 Tm[2][2];
+        row_product(x, Hb, l, h, Tm);
+        // T -> tile (row-major, natural frequency order)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = rowmap(r, h);
+                    W.tile[(s ? 63 - i : i) * kLd + 2 * l + qc] = Tm[s][qc][r];
+                }
+    }
+    WAVE_LDS_SYNC();
+    {
+        // lane L: exact top-k of its row, ties to the lowest index, ascending emission
+        const int L = lane_id();
+        float* trow = W.tile + L * kLd;
+        float yr[64];
+#pragma unroll
+        for (int t = 0; t < 64; ++t) yr[t] = trow[t];
+        uint32_t thr = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t cnd = thr | (1u << bit);
+            int cl = 0;
+#pragma unroll
+            for (int t = 0; t < 64; ++t) cl += fabsf(yr[t]) >= __uint_as_float(cnd - 1u) ? 1 : 0;
+            if (cl >= k) thr = cnd;
+        }
+        int gl = 0;
+#pragma unroll
+        for (int t = 0; t < 64; ++t) gl += keyv(yr[t]) > thr ? 1 : 0;
+        int need = k - gl;
+        int slot = 0;
+        const bool live = L < rows;
+        int32_t* oi = pay_idx + (int64_t)L * k;
+        float* ov = pay_val + (int64_t)L * k;
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+            const uint32_t kv = keyv(yr[t]);
+            const bool tie = kv == thr && need > 0;
+            const bool s = kv > thr || tie;
+            need -= tie ? 1 : 0;
+            if (s && live) {
+                oi[slot] = t;
+                ov[slot] = yr[t];
+            }
+            slot += s ? 1 : 0;
+            trow[t] = s ? yr[t] : 0.f;  // the kept coefficients (Ymask)
+        }
+    }
+    WAVE_LDS_SYNC();
+    {
+        // R^T[c][row] = sum_d F[c][d] Ymask[row][d]; rows l (s = 0) and 63 - l (s = 1)
+        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+        const int c0 = pi_col(0, l), c1 = pi_col(1, l);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const float* yrow = W.tile + (s ? 63 - l : l) * kLd;
+            f32x16 r0 = zero16(), r1 = zero16();
+#pragma unroll
+            for (int t = 0; t < 32; ++t) {
+                const int d = 2 * t + h;
+                const float yv = yrow[d];
+                r0 = mfma(basis64(Hb, c0, d), yv, r0);
+                r1 = mfma(basis64(Hb, c1, d), yv, r1);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[s][q][e] -= (q < 4 ? r0 : r1)[4 * (q & 3) + e];
+        }
+        store_rows(delta, 64, l, h, vec, rows, x);
+    }
+    WAVE_LDS_SYNC();
+    DW_PH(7);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void encode_kernel(
+    const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const ga_demo_rowgroup* __restrict__ groups,
+    int ngroups, const float* __restrict__ F64, T* param0, const T* __restrict__ grad0, T* delta0, int64_t ld,
+    int64_t K, float lr, float decay, float wd_factor, int32_t* payload0, int64_t pstride, int64_t M, int ptr_vec) {
+    __shared__ float Hb[32 * kLd];
+    __shared__ WaveLDS wl[kWaves];
+    for (int q = threadIdx.x; q < 32 * 64; q += kThreads) Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);  // wave-uniform: scalar job loop
+    WaveLDS& W = wl[wid];
+    DW_PH_DECL;
+    const int64_t n64 = (int64_t)nchunks * K;
+    const int64_t total = n64 + (int64_t)ngroups * K;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int tix = -1;
+    int64_t last_rep = -1;
+    for (int64_t job = (int64_t)blockIdx.x * kWaves + wid; job < total; job += stride) {
+        if (job < n64) {
+            const int64_t rep = job / nchunks;
+            const int chunk = (int)(job - rep * nchunks);
+            if (rep != last_rep) {
+                tix = -1;
+                last_rep = rep;
+            }
+            {  // the descriptor of this chunk: advance over chunk_start (wave-wide)
+                const int lane = lane_id();
+                for (;;) {
+                    const int t = tix + 1 + lane;
+                    const uint64_t m = __ballot(t < ntens && tens[t].chunk_start <= chunk);
+                    tix += __popcll(m);
+                    if (m != ~0ull) break;
+                }
+            }
+            const ga_demo_tensor td = tens[tix];
+            const int c = chunk - td.chunk_start;
+            int32_t* pi = payload0 + rep * pstride + td.payload_off + (int64_t)c * td.k;
+            float* pv = reinterpret_cast<float*>(payload0 + rep * pstride + M) + td.payload_off + (int64_t)c * td.k;
+            chunk64<T>(td, c, param0 + rep * ld, grad0 + rep * ld, delta0 + rep * ld, pi, pv, lr, decay, wd_factor,
+                       ptr_vec, Hb, W
+#ifdef GA_DEMO_STAMPS
+                       , ph_acc, ph_last
+#endif
+            );
+            DW_CNT(9);
+        } else {
+            const int64_t j = job - n64;
+            const int64_t rep = j / ngroups;
+            const int g = (int)(j - rep * ngroups);
+            const ga_demo_rowgroup rg = groups[g];
+            rowgroup<T>(rg, param0 + rep * ld, grad0 + rep * ld, delta0 + rep * ld,
+                        payload0 + rep * pstride + rg.payload_off,
+                        reinterpret_cast<float*>(payload0 + rep * pstride + M) + rg.payload_off, lr, decay,
+                        wd_factor, ptr_vec, Hb, W
+#ifdef GA_DEMO_STAMPS
+                        , ph_acc, ph_last
+#endif
+            );
+        }
+    }
+    DW_PH_FLUSH();
+}
+
+template <typename T>
+static int launch(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, const ga_demo_rowgroup* groups,
+                  int32_t ngroups, const float* F64, void* param, const void* grad, void* delta, int64_t K,
+                  int64_t ld, float lr, float decay, float wd_factor, int32_t* payload, int64_t pstride, int64_t M,
+                  int ptr_vec, hipStream_t stream) {
+    auto kern = encode_kernel<T>;
+    static const int resident = [&] {
+        int per_cu = 0, dev = 0, cus = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
+    }();
+    const int64_t jobs = ((int64_t)nchunks + ngroups) * K;
+    const int64_t want = (jobs + kWaves - 1) / kWaves;
+    const int grid = (int)(want < resident ? want : resident);
+    if (grid <= 0) return GA_OK;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks, groups, ngroups, F64,
+                       (T*)param, (const T*)grad, (T*)delta, ld, K, lr, decay, wd_factor, payload, pstride, M,
+                       ptr_vec);
+    return GA_OK;
+}
+
+#ifdef GA_DEMO_STAMPS
+__device__ unsigned long long* g_demo_stamps_w;
+#endif
+
+}  // namespace dw
+}  // namespace ga
+
+using namespace ga;
+
+#ifdef GA_DEMO_STAMPS
+extern "C" GA_API int ga_demo_stamps_set_wave(unsigned long long* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(ga::dw::g_demo_stamps_w), &buf, sizeof(buf)) == hipSuccess ? 0 : 2;
+}
+#endif
+
+extern "C" GA_API int ga_demo_encode_sym(int dtype, const ga_demo_tensor* tensors, int32_t ntensors,
+                                         int32_t nchunks, const ga_demo_rowgroup* groups, int32_t ngroups,
+                                         const float* F64, void* param, const void* grad, void* delta, int64_t K,
+                                         int64_t ld, float lr, float decay, float wd_factor, int32_t* payload,
+                                         int64_t payload_stride, int64_t M, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(ntensors >= 0 && nchunks >= 0 && ngroups >= 0 && (nchunks > 0 || ngroups > 0),
+               "ga_demo_encode_sym: empty plan (ntensors=%d nchunks=%d ngroups=%d)", ntensors, nchunks, ngroups);
+    GA_REQUIRE(nchunks == 0 || (tensors && ntensors >= 1), "ga_demo_encode_sym: no descriptors");
+    GA_REQUIRE(ngroups == 0 || groups, "ga_demo_encode_sym: no row groups");
+    GA_REQUIRE(F64 && param && grad && delta && payload, "ga_demo_encode_sym: null buffer");
+    GA_REQUIRE(K >= 1 && ((int64_t)nchunks + ngroups) * K < (1ll << 40), "ga_demo_encode_sym: K=%lld out of range",
+               (long long)K);
+    GA_REQUIRE(K == 1 || (ld > 0 && payload_stride >= 2 * M), "ga_demo_encode_sym: bad replica strides");
+    const int vb = dtype == GA_F32 ? 16 : 8;
+    const int ptr_vec = ((uintptr_t)param % vb == 0) && ((uintptr_t)grad % vb == 0) &&
+                        ((uintptr_t)delta % vb == 0) && (K == 1 || ld % 4 == 0);
+    switch (dtype) {
+        case GA_F32:
+            dw::launch<float>(tensors, ntensors, nchunks, groups, ngroups, F64, param, grad, delta, K, ld, lr, decay,
+                              wd_factor, payload, payload_stride, M, ptr_vec, stream);
+            break;
+        case GA_BF16:
+            dw::launch<__hip_bfloat16>(tensors, ntensors, nchunks, groups, ngroups, F64, param, grad, delta, K, ld,
+                                       lr, decay, wd_factor, payload, payload_stride, M, ptr_vec, stream);
+            break;
+        default: set_error("ga_demo_encode_sym: unknown dtype %d", dtype); return GA_EINVAL;
+    }
+    return check_launch("ga_demo_encode_sym");
+}

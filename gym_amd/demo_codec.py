@@ -12,7 +12,7 @@ import math
 import numpy as np
 import torch
 
-from ._lib import DemoTensor
+from ._lib import DemoRowGroup, DemoTensor
 
 TILE = 64
 
@@ -103,6 +103,28 @@ class DemoPlan:
             raise ValueError("DeMo: too many chunks for one launch")
         self.ntensors = len(descs)
         self.nchunks = chunk_start
+        # every chunk 64x64 or 1x64 with k <= 64: the wave-per-chunk encode applies
+        # (ga_demo_encode_sym: the 64x64 tensors re-numbered, the 1x64 chunks in row groups)
+        self.wave_encode = all(d.n2 == TILE and d.n1 in (1, TILE) and d.k <= 64 for d in descs)
+        self._wave_host = None
+        if self.wave_encode:
+            d64, groups, start = [], [], 0
+            for d in descs:
+                if d.n1 == TILE:
+                    d64.append(DemoTensor(offset=d.offset, payload_off=d.payload_off, rows=d.rows, cols=d.cols,
+                                          n1=d.n1, n2=d.n2, gy=d.gy, gx=d.gx, k=d.k, basis1=d.basis1,
+                                          basis2=d.basis2, chunk_start=start))
+                    start += d.gy * d.gx
+                else:  # 1x64 chunk c of this tensor at offset + 64c (codec_view: C = 64 gx)
+                    nch = d.gy * d.gx
+                    for c0 in range(0, nch, TILE):
+                        groups.append(DemoRowGroup(offset=d.offset + TILE * c0, payload_off=d.payload_off + c0 * d.k,
+                                                   rows=min(TILE, nch - c0), k=d.k))
+            a64 = (DemoTensor * max(1, len(d64)))(*d64)
+            ag = (DemoRowGroup * max(1, len(groups)))(*groups)
+            self.n64tensors, self.n64chunks, self.ngroups = len(d64), start, len(groups)
+            self._wave_host = (torch.frombuffer(bytearray(bytes(a64)), dtype=torch.uint8),
+                               torch.frombuffer(bytearray(bytes(ag)), dtype=torch.uint8))
         self.M = payload_off
         self.n_arena = layout.n
         arr = (DemoTensor * len(descs))(*descs)
@@ -114,8 +136,10 @@ class DemoPlan:
         # the inverse of an orthonormal basis is its transpose (idct(eye(n)), demo.py:398-442)
         self._B_host = torch.from_numpy(np.ascontiguousarray(F.transpose(0, 2, 1)).astype(np.float32))
         self.basis_sizes = sizes
+        self._F64_host = self._F_host[basis_of[TILE]].contiguous() if TILE in basis_of else None
         self.device = None
         self.desc = self.F = self.B = None
+        self.desc64 = self.groups = self.F64 = None
 
     def to(self, device):
         device = torch.device(device)
@@ -123,6 +147,9 @@ class DemoPlan:
             self.desc = self._desc_host.to(device)
             self.F = self._F_host.to(device)
             self.B = self._B_host.to(device)
+            if self._wave_host is not None:
+                self.desc64, self.groups = (t.to(device) for t in self._wave_host)
+                self.F64 = self._F64_host.to(device)
             self.device = device
         return self
 

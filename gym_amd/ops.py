@@ -8,6 +8,7 @@ a CPU tensor raises.
 Replica sets are 2-D tensors [K, ld]; a 1-D tensor is one replica.
 """
 import ctypes
+import os
 
 import torch
 
@@ -169,6 +170,13 @@ def demo_encode(plan, param, grad, delta, payload, lr, decay, wd_factor):
     if pl2.dtype != torch.int32 or pl2.shape[0] != K or pl2.shape[1] < 2 * plan.M:
         raise ValueError("demo_encode: payload must be int32 [K, >= 2*M]")
     plan.to(p2.device)
+    # 64x64 / 1x64 chunks with k <= 64: the wave-per-chunk kernel (GA_DEMO_ENCODE=block forces the other)
+    if plan.wave_encode and os.environ.get("GA_DEMO_ENCODE") != "block":
+        check(lib().ga_demo_encode_sym(_dtype_code(p2), _p(plan.desc64), plan.n64tensors, plan.n64chunks,
+                                       _p(plan.groups), plan.ngroups, _p(plan.F64), _p(p2), _p(g2), _p(d2), K, ld,
+                                       float(lr), float(decay), float(wd_factor), _p(pl2), pl2.stride(0), plan.M,
+                                       _stream()), "ga_demo_encode_sym")
+        return
     check(lib().ga_demo_encode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.F), _p(plan.B),
                                _p(p2), _p(g2), _p(d2), K, ld, float(lr), float(decay), float(wd_factor), _p(pl2),
                                pl2.stride(0), plan.M, _stream()), "ga_demo_encode")

@@ -190,6 +190,35 @@ GA_API int ga_demo_encode(int dtype, const ga_demo_tensor* tensors, int32_t nten
                           hipStream_t stream);
 
 /*
+ * Up to 64 consecutive 1x64 chunks of one tensor (rows of a vector's chunk
+ * view): element offset of the first chunk, payload entry offset of its
+ * entries, number of chunks, entries per chunk.
+ */
+typedef struct ga_demo_rowgroup {
+    int64_t offset;
+    int64_t payload_off;
+    int32_t rows;
+    int32_t k;
+} ga_demo_rowgroup;
+
+/*
+ * ga_demo_encode (demo.py:142-209 encode + compress + residual) for plans whose
+ * chunks are all 64x64 or 1x64 with k <= 64 -- compression_chunk = 64 on
+ * GPT-2-shaped models: same arithmetic, payload layout and tie rule.  The
+ * 64x64 chunks are described by `tensors` (only 64x64 tensors, chunk_start
+ * counting those chunks, payload_off as in the full plan), the 1x64 chunks by
+ * `groups`; F64 is the 64-point basis F[i][k] (64x64 fp32).  One wavefront per
+ * chunk (or row group), operands register-resident, the DCT products folded by
+ * the symmetry F[63-i][k] = (-1)^k F[i][k].
+ */
+GA_API int ga_demo_encode_sym(int dtype, const ga_demo_tensor* tensors, int32_t ntensors,
+                              int32_t nchunks, const ga_demo_rowgroup* groups, int32_t ngroups,
+                              const float* F64, void* param, const void* grad, void* delta,
+                              int64_t K, int64_t ld, float lr, float decay, float wd_factor,
+                              int32_t* payload, int64_t payload_stride, int64_t M,
+                              hipStream_t stream);
+
+/*
  * Decode the gathered payloads of S sources (source s at payload + s*payload_stride,
  * in node order), scatter-mean them per chunk (mean over the entries that hit a
  * coefficient, demo.py:331-352), inverse DCT (B1^T . X . B2), sign, and apply the

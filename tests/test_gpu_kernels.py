@@ -290,6 +290,8 @@ def test_sparta_mask_mode_matches_reference_golden(golden, K):
 
 # ---------------------------------------------------------------- DeMo --------
 DEMO_SHAPES = [(128, 128), (66, 128), (768,), (8, 4, 3, 3), (10,), (58, 29), (64, 64)]
+# every chunk 64x64 or 1x64: the plan takes the wave-per-chunk encode (ga_demo_encode_sym)
+DEMO_WAVE_SHAPES = [(128, 128), (768,), (64, 64), (192, 128), (320,), (64, 192)]
 
 
 def _demo_setup(shapes, K, seed=0, dtype=torch.float32):
@@ -315,11 +317,12 @@ def _payload_host(pl, plan):
     return a[:, : plan.M], a[:, plan.M: 2 * plan.M].view(np.float32)
 
 
-@pytest.mark.parametrize("K", [1, 2, 3, 5])
-def test_demo_encode_decode_matches_oracle(K):
+@pytest.mark.parametrize("K,wave", [(1, False), (2, False), (3, False), (5, False), (1, True), (3, True)])
+def test_demo_encode_decode_matches_oracle(K, wave):
     from gym_amd import ops
-    shapes = DEMO_SHAPES
+    shapes = DEMO_WAVE_SHAPES if wave else DEMO_SHAPES
     L, plan, a = _demo_setup(shapes, K, seed=K)
+    assert plan.wave_encode == wave
     lr, decay, wd = 0.01, 0.999, 0.1
     wdf = float(np.float32(1.0 - lr * wd))
     P, G, D = t(a["p"]), t(a["g"]), t(a["d"])
@@ -407,12 +410,16 @@ def test_demo_matches_reference_golden_steps(golden):
                 np.testing.assert_allclose(host(L.views(D[k])[i]), ref_d, rtol=0, atol=2e-5 * scale)
 
 
-def test_demo_all_zero_chunk_tie_rule():
+@pytest.mark.parametrize("kernel", ["wave", "block"])
+def test_demo_all_zero_chunk_tie_rule(monkeypatch, kernel):
     from gym_amd import ops
     from gym_amd.arena import ArenaLayout
     from gym_amd.demo_codec import DemoPlan
+    if kernel == "block":
+        monkeypatch.setenv("GA_DEMO_ENCODE", "block")
     L = ArenaLayout([(128, 128)])
     plan = DemoPlan(L)
+    assert plan.wave_encode
     P = torch.zeros(1, L.n, device=DEV)
     payload = torch.full((1, 2 * plan.M), -1, dtype=torch.int32, device=DEV)
     ops.demo_encode(plan, P, P.clone(), P.clone(), payload, 0.01, 0.999, 1.0)
@@ -421,15 +428,18 @@ def test_demo_all_zero_chunk_tie_rule():
     assert all(np.array_equal(idx[0, c * 32:(c + 1) * 32], np.arange(32)) for c in range(4))
 
 
-@pytest.mark.parametrize("topk,chunk", [(300, 64), (8, 16), (64, 32)])
-def test_demo_topk_and_chunk_variants(topk, chunk):
-    """k > 256 (radix-select path), small chunks, k == chunk."""
+@pytest.mark.parametrize("topk,chunk,wave", [(300, 64, False), (8, 16, False), (64, 32, False), (1, 64, True),
+                                             (8, 64, True), (48, 64, True), (64, 64, True), (65, 64, False)])
+def test_demo_topk_and_chunk_variants(topk, chunk, wave):
+    """k > 256 (radix-select path), small chunks, k == chunk; the wave kernel's
+    k range (k <= 64; k > 32 mostly takes its all-keys selection)."""
     from gym_amd import ops
     from gym_amd.arena import ArenaLayout
     from gym_amd.demo_codec import DemoPlan
-    shapes = [(128, 128), (96,), (32, 48)]
+    shapes = [(128, 128), (192,), (64, 128)] if chunk == 64 and topk <= 65 else [(128, 128), (96,), (32, 48)]
     L = ArenaLayout(shapes)
     plan = DemoPlan(L, chunk=chunk, topk=topk)
+    assert plan.wave_encode == wave
     rng = np.random.default_rng(topk + chunk)
     D = np.zeros((1, L.n), np.float32)
     for o, nel in zip(L.offsets, L.numels):
@@ -454,9 +464,9 @@ def test_demo_topk_and_chunk_variants(topk, chunk):
         e0 += ne
 
 
-def test_demo_bf16_matches_oracle():
+@pytest.mark.parametrize("shapes", [[(128, 128), (768,), (66, 128)], [(128, 128), (768,)]])
+def test_demo_bf16_matches_oracle(shapes):
     from gym_amd import ops
-    shapes = [(128, 128), (768,), (66, 128)]
     L, plan, a = _demo_setup(shapes, 2, seed=11)
     lr = 0.01
     P = t(a["p"], torch.bfloat16)

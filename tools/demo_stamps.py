@@ -23,8 +23,14 @@ PHASES = ["error-feedback+prefetch", "DCT product 1", "DCT product 2", "top-k se
           "delta store"]
 
 
+WAVE_PHASES = ["64x64: load+error feedback", "64x64: row product+park", "64x64: column product",
+               "64x64: top-k", "64x64: residual", "64x64: delta store", "row groups: load", "row groups: rest"]
+
+
 def main():
-    model = sys.argv[1] if len(sys.argv) > 1 else "gpt2-350m"
+    wave = "--wave" in sys.argv
+    argv = [a for a in sys.argv[1:] if a != "--wave"]
+    model = argv[0] if argv else "gpt2-350m"
     L = ctypes.CDLL(os.path.join(ROOT, "build", "libgym_amd_stamps.so"))
     for name, (res, args) in _lib.SIGNATURES.items():
         f = getattr(L, name)
@@ -41,12 +47,24 @@ def main():
     assert L.ga_demo_stamps_set(ctypes.c_void_p(stamps.data_ptr())) == 0
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
+    if wave:
+        assert plan.wave_encode, "the plan does not qualify for ga_demo_encode_sym"
+        L.ga_demo_stamps_set_wave.argtypes = [ctypes.c_void_p]
+        assert L.ga_demo_stamps_set_wave(ctypes.c_void_p(stamps.data_ptr())) == 0
+
     def run():
-        rc = L.ga_demo_encode(0, ctypes.c_void_p(plan.desc.data_ptr()), plan.ntensors, plan.nchunks,
-                              ctypes.c_void_p(plan.F.data_ptr()), ctypes.c_void_p(plan.B.data_ptr()),
-                              ctypes.c_void_p(P.data_ptr()), ctypes.c_void_p(G.data_ptr()),
-                              ctypes.c_void_p(D.data_ptr()), 1, layout.n, 1e-3, 0.999, 1.0,
-                              ctypes.c_void_p(pl.data_ptr()), 2 * plan.M, plan.M, s)
+        if wave:
+            rc = L.ga_demo_encode_sym(0, ctypes.c_void_p(plan.desc64.data_ptr()), plan.n64tensors, plan.n64chunks,
+                                      ctypes.c_void_p(plan.groups.data_ptr()), plan.ngroups,
+                                      ctypes.c_void_p(plan.F64.data_ptr()), ctypes.c_void_p(P.data_ptr()),
+                                      ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(D.data_ptr()), 1, layout.n,
+                                      1e-3, 0.999, 1.0, ctypes.c_void_p(pl.data_ptr()), 2 * plan.M, plan.M, s)
+        else:
+            rc = L.ga_demo_encode(0, ctypes.c_void_p(plan.desc.data_ptr()), plan.ntensors, plan.nchunks,
+                                  ctypes.c_void_p(plan.F.data_ptr()), ctypes.c_void_p(plan.B.data_ptr()),
+                                  ctypes.c_void_p(P.data_ptr()), ctypes.c_void_p(G.data_ptr()),
+                                  ctypes.c_void_p(D.data_ptr()), 1, layout.n, 1e-3, 0.999, 1.0,
+                                  ctypes.c_void_p(pl.data_ptr()), 2 * plan.M, plan.M, s)
         assert rc == 0, L.ga_last_error()
 
     for _ in range(3):
@@ -58,6 +76,17 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     st = stamps.view(-1, 16).cpu().numpy().astype(np.int64)
+    if wave:  # one row per wave: 7 phase sums, [8] all-keys selections, [9] chunks
+        st = st[st[:, 9] > 0]
+        tot = st[:, :8].sum(axis=1)
+        nch = st[:, 9]
+        print(f"{model}: {plan.nchunks} chunks over {len(st)} waves, kernel {e0.elapsed_time(e1):.3f} ms "
+              f"(stamped build); all-keys selections {st[:, 8].sum()} of {nch.sum()} chunks")
+        print(f"cycles per chunk (wave view): median {np.median(tot / nch):.0f}")
+        for i, name in enumerate(WAVE_PHASES):
+            v = st[:, i] / nch
+            print(f"  {name:22s} median {np.median(v):8.0f} cyc/chunk  share {np.median(st[:, i] / tot):6.1%}")
+        return
     st = st[st[:, 8] > 0]  # workgroups that ran (persistent grid)
     tot = st[:, :6].sum(axis=1)
     nch = st[:, 8]
