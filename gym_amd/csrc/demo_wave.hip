@@ -43,7 +43,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #ifdef GA_DEMO_STAMPS
 extern __device__ unsigned long long* g_demo_stamps_w;
-#define DW_PH_DECL unsigned long long ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, ph_last = __builtin_amdgcn_s_memtime()
+#define DW_PH_DECL unsigned long long ph_acc[16] = {}, ph_last = __builtin_amdgcn_s_memtime()
 #define DW_PH(i)                                                    \
     do {                                                            \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -55,7 +55,7 @@ extern __device__ unsigned long long* g_demo_stamps_w;
     do {                                                                                                    \
         if ((threadIdx.x & 63) == 0) {                                                                      \
             unsigned long long* row_ = g_demo_stamps_w + ((size_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 16; \
-            for (int i_ = 0; i_ < 10; ++i_) row_[i_] = ph_acc[i_];                                          \
+            for (int i_ = 0; i_ < 16; ++i_) row_[i_] = ph_acc[i_];                                          \
         }                                                                                                   \
     } while (0)
 #else
@@ -104,19 +104,34 @@ __device__ __forceinline__ float basis64(const float* Hb, int i, int d) {
 
 __device__ __forceinline__ uint32_t keyv(float v) { return (__float_as_uint(v) & 0x7fffffffu) + 1u; }
 
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+// exclusive prefix sum over the wave of a per-lane value 0 <= v < 128, bit-sliced:
+// ballots and mbcnt only (no LDS round trips)
+__device__ __forceinline__ int wave_excl_scan128(int v) {
+    int r = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(v, d, 64);
-        if (lane >= d) v += y;
+    for (int b = 0; b < 7; ++b) {
+        const uint64_t m = __ballot((v >> b) & 1);
+        r += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
     }
-    return v;
+    return r;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
+}
+
+// Largest descriptor index t >= max(tix, 0) with chunk_start <= chunk (chunk_start
+// increases): a uniform binary search on scalar loads (no vector memory operation)
+__device__ __forceinline__ int find_tensor(const ga_demo_tensor* __restrict__ T, int ntens, int tix, int chunk) {
+    int lo = tix < 0 ? 0 : tix, hi = ntens - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (T[mid].chunk_start <= chunk) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
 }
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int j) {
@@ -133,11 +148,20 @@ struct WaveLDS {
 // ---- operands in registers --------------------------------------------------
 // x[s][q][e]: row l (s = 0) or 63 - l (s = 1), column 4 blk(h, q) + e
 // lane offset of x[s][q][0] from the chunk's (0, 0) element (32-bit: a chunk spans < 2^31 elements)
-__device__ __forceinline__ int lane_off(int s, int q, int l, int h, int stride) {
-    return (s ? 63 - l : l) * stride + 4 * blk(h, q);
+__device__ __forceinline__ uint32_t lane_off(int s, int q, int l, int h, int stride) {
+    return (uint32_t)((s ? 63 - l : l) * stride + 4 * blk(h, q));
 }
 
-// pb: the chunk's (0, 0) element (wave-uniform pointer; the lane part is a 32-bit offset)
+// uniform base + zero-extended 32-bit lane byte offset: global_load/store with an SGPR base
+template <typename T>
+__device__ __forceinline__ const T* at_off(const T* pb, uint32_t off) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(pb) + (uint64_t)(uint32_t)(off * (uint32_t)sizeof(T)));
+}
+template <typename T>
+__device__ __forceinline__ T* at_off(T* pb, uint32_t off) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(pb) + (uint64_t)(uint32_t)(off * (uint32_t)sizeof(T)));
+}
+
 template <typename T>
 __device__ __forceinline__ void load_rows(const T* pb, int stride, int l, int h, bool vec, int nrows,
                                           float (&o)[2][8][4]) {
@@ -146,7 +170,7 @@ __device__ __forceinline__ void load_rows(const T* pb, int stride, int l, int h,
         for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(pb + lane_off(s, q, l, h, stride)),
+                Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, lane_off(s, q, l, h, stride))),
                                 o[s][q]);
         return;
     }
@@ -155,7 +179,7 @@ __device__ __forceinline__ void load_rows(const T* pb, int stride, int l, int h,
         const bool live = (s ? 63 - l : l) < nrows;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const T* a = pb + lane_off(s, q, l, h, stride);
+            const T* a = at_off(pb, lane_off(s, q, l, h, stride));
             if (live && vec) {
                 Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(a), o[s][q]);
             } else {
@@ -174,7 +198,7 @@ __device__ __forceinline__ void store_rows(T* pb, int stride, int l, int h, bool
         for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                *reinterpret_cast<typename Vec4<T>::type*>(pb + lane_off(s, q, l, h, stride)) = Vec4<T>::pack(o[s][q]);
+                *reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, lane_off(s, q, l, h, stride))) = Vec4<T>::pack(o[s][q]);
         return;
     }
 #pragma unroll
@@ -182,7 +206,7 @@ __device__ __forceinline__ void store_rows(T* pb, int stride, int l, int h, bool
         if ((s ? 63 - l : l) >= nrows) continue;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            T* a = pb + lane_off(s, q, l, h, stride);
+            T* a = at_off(pb, lane_off(s, q, l, h, stride));
             if (vec) {
                 *reinterpret_cast<typename Vec4<T>::type*>(a) = Vec4<T>::pack(o[s][q]);
             } else {
@@ -242,12 +266,55 @@ __device__ __forceinline__ void row_product(const float (&x)[2][8][4], const flo
 }
 
 // ---- 64x64 chunk ------------------------------------------------------------
+// Global memory is read and written in the coalesced layout C -- lane t holds rows
+// (t >> 4) + 4i (i < 16), 4 elements at column 4 (t & 15): each access covers 4
+// whole 256-byte row segments -- and the chunk goes through the LDS tile into the
+// row-pair layout of the products (a direct row-pair access touches 64 lines per
+// instruction and runs ~20% slower).
+__device__ __forceinline__ uint32_t coal_off(int i, int lane, int stride) {
+    return (uint32_t)(((lane >> 4) + 4 * i) * stride + 4 * (lane & 15));
+}
+
+template <typename T>
+__device__ __forceinline__ void load_coal(const T* pb, int stride, bool vec, int lane, float (&o)[16][4]) {
+    if (vec) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride))),
+                            o[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[i][e] = Elem<T>::load(at_off(pb, coal_off(i, lane, stride)) + e);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_coal(T* pb, int stride, bool vec, int lane, const float (&o)[16][4]) {
+    if (vec) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            *reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride))) = Vec4<T>::pack(o[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Elem<T>::store(at_off(pb, coal_off(i, lane, stride)) + e, o[i][e]);
+    }
+}
+
+// float4 index of (row, column block cb) in the chunk tile: row-major, blocks XOR-swizzled
+// by row, so whole-row (layout C) and row-pair (l, h) accesses are both bank-conflict free
+__device__ __forceinline__ int t4(int row, int cb) { return row * 16 + (cb ^ (row & 15)); }
+
+
 template <typename T>
 __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* param, const T* grad, T* delta,
                                         int32_t* out_idx, float* out_val, float lr, float decay, float wd_factor,
                                         int ptr_vec, const float* Hb, WaveLDS& W
 #ifdef GA_DEMO_STAMPS
-                                        , unsigned long long (&ph_acc)[10], unsigned long long& ph_last
+                                        , unsigned long long (&ph_acc)[16], unsigned long long& ph_last
 #endif
 ) {
     const int k = td.k;
@@ -257,23 +324,47 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
     grad += base;
     delta += base;
     const bool vec = ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0);
-    float4* park = reinterpret_cast<float4*>(W.tile);  // x while the products and the top-k run
-    float x[2][8][4];
+    float4* tile = reinterpret_cast<float4*>(W.tile);  // x, then delta, in the swizzled row-major layout
     {
-        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-        error_feedback(param, grad, delta, td.cols, l, h, vec, 64, lr, decay, wd_factor, x);
+        const int lane = lane_id();
+        if (wd_factor != 1.f) {  // decoupled weight decay of p (demo.py:159-160), its own pass
+            float pv[16][4];
+            load_coal(param, td.cols, vec, lane, pv);
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pv[i][e] *= wd_factor;
+            store_coal(param, td.cols, vec, lane, pv);
+        }
+        float Dv[16][4], Gv[16][4];
+        load_coal(delta, td.cols, vec, lane, Dv);
+        load_coal(grad, td.cols, vec, lane, Gv);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaf(lr, Gv[i][e], decay != 1.f ? Dv[i][e] * decay : Dv[i][e]);
+            tile[t4((lane >> 4) + 4 * i, lane & 15)] = make_float4(v[0], v[1], v[2], v[3]);
+        }
     }
+    WAVE_LDS_SYNC();
     DW_PH(0);
     f32x16 Y[2][2];  // [parity of b][qc]
     {
         const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-        f32x16 Tm[2][2];
-        row_product(x, Hb, l, h, Tm);
+        float x[2][8][4];
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                park[(8 * s + q) * 64 + lane] = make_float4(x[s][q][0], x[s][q][1], x[s][q][2], x[s][q][3]);
+            for (int q = 0; q < 8; ++q) {
+                const float4 v = tile[t4(s ? 63 - l : l, blk(h, q))];
+                x[s][q][0] = v.x;
+                x[s][q][1] = v.y;
+                x[s][q][2] = v.z;
+                x[s][q][3] = v.w;
+            }
+        f32x16 Tm[2][2];
+        row_product(x, Hb, l, h, Tm);
         DW_PH(1);
 #pragma unroll
         for (int qc = 0; qc < 2; ++qc) {
@@ -320,13 +411,15 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
         for (int qc = 0; qc < 2; ++qc)
 #pragma unroll
             for (int r = 0; r < 16; ++r) mine += fabsf(Y[par][qc][r]) >= T0f ? 1 : 0;
-    const int incl = wave_incl_scan(mine, lane);
+    const int excl = wave_excl_scan128(mine);  // mine <= 64
+    const int incl = excl + mine;
     const int C = __builtin_amdgcn_readlane(incl, 63);
+    DW_PH(10);
     W.bm[2 * lane] = 0u;
     W.bm[2 * lane + 1] = 0u;
     if (C <= kCand) {
         // compact the candidates: (pos, bits) at the lane's next slot, others to its discard slot
-        int at = incl - mine;
+        int at = excl;
         uint2* L2 = reinterpret_cast<uint2*>(W.lst);
         float T0c = T0f;  // an opaque copy: the 64 compares are redone here, not kept as 64 lane masks
         asm volatile("" : "+v"(T0c));
@@ -342,6 +435,7 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
                     at += cnd ? 1 : 0;
                 }
         WAVE_LDS_SYNC();
+        DW_PH(11);
         uint32_t pos[2], bits[2], key[2];
         bool ok[2];
 #pragma unroll
@@ -358,7 +452,7 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
         // rank of a candidate = candidates at lower positions (bitmap prefix counts)
         const uint32_t w0 = W.bm[2 * lane], w1 = W.bm[2 * lane + 1];
         const int cnt = __popc(w0) + __popc(w1);
-        const int pre = wave_incl_scan(cnt, lane) - cnt;
+        const int pre = wave_excl_scan128(cnt);  // cnt <= 64
         int rank[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -368,6 +462,7 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
             const int preL = __shfl(pre, Lw, 64);
             rank[e] = ok[e] ? preL + __popcll(pair & ((1ull << (pos[e] & 63)) - 1ull)) : 0x7fff;
         }
+        DW_PH(12);
         // exact k-th key among the candidates
         uint32_t thr = 0;
         for (int bit = 31; bit >= 0; --bit) {
@@ -395,6 +490,7 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
             sel[0] = key[0] > thr || (key[0] == thr && tr[0] < need);
             sel[1] = key[1] > thr || (key[1] == thr && tr[1] < need);
         }
+        DW_PH(13);
         if (lane < 4) W.sm[lane] = 0u;
         WAVE_LDS_SYNC();
 #pragma unroll
@@ -449,7 +545,7 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
         WAVE_LDS_SYNC();
         uint32_t w0 = W.bm[2 * lane], w1 = W.bm[2 * lane + 1];
         int cnt = __popc(w0) + __popc(w1);
-        int pre = wave_incl_scan(cnt, lane) - cnt;
+        int pre = wave_excl_scan128(cnt);
         WAVE_LDS_SYNC();
         W.bm[2 * lane] = 0u;  // becomes the selection bitmap
         W.bm[2 * lane + 1] = 0u;
@@ -473,7 +569,7 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
         w0 = W.bm[2 * lane];
         w1 = W.bm[2 * lane + 1];
         cnt = __popc(w0) + __popc(w1);
-        pre = wave_incl_scan(cnt, lane) - cnt;
+        pre = wave_excl_scan128(cnt);
 #pragma unroll
         for (int par = 0; par < 2; ++par)
 #pragma unroll
@@ -497,57 +593,70 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
         WAVE_LDS_SYNC();
     }
     DW_PH(3);
-    // ---- residual (demo.py:174-180) in the load layout: R^T per parity of b
-    const uint32_t epos = lane < k ? W.lst[2 * lane] : 0u;
-    const uint32_t ebits = lane < k ? W.lst[2 * lane + 1] : 0u;
-    f32x16 R[2][2];  // [parity][column half H]
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-        R[par][0] = zero16();
-        R[par][1] = zero16();
-        uint64_t mk = __ballot(lane < k && (int)((epos >> 6) & 1u) == par);
-        const int c0 = pi_col(0, l), c1 = pi_col(1, l);
-        while (mk) {
-            const int j0 = __builtin_ctzll(mk);
-            mk &= mk - 1;
-            uint32_t p1 = 0u, v1 = 0u;
-            const uint32_t p0 = rdl(epos, j0), v0 = rdl(ebits, j0);
-            if (mk) {
-                const int j1 = __builtin_ctzll(mk);
-                mk &= mk - 1;
-                p1 = rdl(epos, j1);
-                v1 = rdl(ebits, j1);
-            }
-            const uint32_t pe = h ? p1 : p0;
-            const float ve = __uint_as_float(h ? v1 : v0);
-            const int bq = (int)(pe >> 6), dq = (int)(pe & 63);
-            const float bop = Hb[l * kLd + bq];  // F[l][b_e]
-            R[par][0] = mfma(ve * basis64(Hb, c0, dq), bop, R[par][0]);
-            R[par][1] = mfma(ve * basis64(Hb, c1, dq), bop, R[par][1]);
-        }
+    // ---- residual (demo.py:174-180) in the load layout: R^T per parity of b, one
+    //      column half H at a time
+    uint2* lstp = reinterpret_cast<uint2*>(W.lst);  // [parity][64] entries
+    int np0, np1;
+    {
+        const uint32_t epos = lane < k ? W.lst[2 * lane] : 0u;
+        const uint32_t ebits = lane < k ? W.lst[2 * lane + 1] : 0u;
+        const int pl = (int)((epos >> 6) & 1u);
+        const uint64_t m0 = __ballot(lane < k && pl == 0), m1 = __ballot(lane < k && pl == 1);
+        const uint64_t mm = pl ? m1 : m0;
+        const int ix = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+        const int E0 = __popcll(m0), E1 = __popcll(m1);
+        WAVE_LDS_SYNC();
+        if (lane < k) lstp[pl * 64 + ix] = make_uint2(epos, ebits);
+        if (lane == 0 && (E0 & 1)) lstp[E0] = make_uint2(0u, 0u);  // odd count: a zero partner
+        if (lane == 1 && (E1 & 1)) lstp[64 + E1] = make_uint2(0u, 0u);
+        WAVE_LDS_SYNC();
+        np0 = (E0 + 1) >> 1;
+        np1 = (E1 + 1) >> 1;
     }
-    DW_PH(4);
-    // delta = x - R: row l gets Re + Ro, row 63 - l gets Re - Ro
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const float4 v = park[(8 * s + q) * 64 + lane];
-            x[s][q][0] = v.x;
-            x[s][q][1] = v.y;
-            x[s][q][2] = v.z;
-            x[s][q][3] = v.w;
+    for (int H = 0; H < 2; ++H) {
+        const int cH = pi_col(H, l);
+        f32x16 Re = zero16(), Ro = zero16();
+        for (int q = 0; q < np0; ++q) {  // lane half h takes entry 2q + h
+            const uint2 e = lstp[2 * q + h];
+            const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
+            Re = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Re);
         }
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int Hh = q >> 2, r = 4 * (q & 3) + e;
-            const float re = R[0][Hh][r], ro = R[1][Hh][r];
-            x[0][q][e] -= re + ro;
-            x[1][q][e] -= re - ro;
+        for (int q = 0; q < np1; ++q) {
+            const uint2 e = lstp[64 + 2 * q + h];
+            const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
+            Ro = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Ro);
         }
-    store_rows(delta, td.cols, l, h, vec, 64, x);
+        // delta = x - R in the tile, at the lane's own blocks 4H .. 4H+3: row l gets
+        // Re + Ro, row 63 - l gets Re - Ro
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                float4& v = tile[t4(s ? 63 - l : l, blk(h, 4 * H + qq))];
+                float4 o = v;
+                const int r = 4 * qq;
+                o.x -= s ? Re[r] - Ro[r] : Re[r] + Ro[r];
+                o.y -= s ? Re[r + 1] - Ro[r + 1] : Re[r + 1] + Ro[r + 1];
+                o.z -= s ? Re[r + 2] - Ro[r + 2] : Re[r + 2] + Ro[r + 2];
+                o.w -= s ? Re[r + 3] - Ro[r + 3] : Re[r + 3] + Ro[r + 3];
+                v = o;
+            }
+        DW_PH(4);
+    }
+    WAVE_LDS_SYNC();
+    {  // delta, coalesced
+        float o[16][4];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+            o[i][0] = v.x;
+            o[i][1] = v.y;
+            o[i][2] = v.z;
+            o[i][3] = v.w;
+        }
+        store_coal(delta, td.cols, vec, lane, o);
+    }
     WAVE_LDS_SYNC();
     DW_PH(5);
 }
@@ -558,7 +667,7 @@ __device__ __forceinline__ void rowgroup(const ga_demo_rowgroup& rg, T* param, c
                                          int32_t* pay_idx, float* pay_val, float lr, float decay,
                                          float wd_factor, int ptr_vec, const float* Hb, WaveLDS& W
 #ifdef GA_DEMO_STAMPS
-                                         , unsigned long long (&ph_acc)[10], unsigned long long& ph_last
+                                         , unsigned long long (&ph_acc)[16], unsigned long long& ph_last
 #endif
 ) {
     const int rows = rg.rows, k = rg.k;
@@ -669,23 +778,16 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int tix = -1;
     int64_t last_rep = -1;
-    for (int64_t job = (int64_t)blockIdx.x * kWaves + wid; job < total; job += stride) {
-        if (job < n64) {
+    int64_t job = (int64_t)blockIdx.x * kWaves + wid;
+    for (; job < n64; job += stride) {  // 64x64 chunks
+        {
             const int64_t rep = job / nchunks;
             const int chunk = (int)(job - rep * nchunks);
             if (rep != last_rep) {
                 tix = -1;
                 last_rep = rep;
             }
-            {  // the descriptor of this chunk: advance over chunk_start (wave-wide)
-                const int lane = lane_id();
-                for (;;) {
-                    const int t = tix + 1 + lane;
-                    const uint64_t m = __ballot(t < ntens && tens[t].chunk_start <= chunk);
-                    tix += __popcll(m);
-                    if (m != ~0ull) break;
-                }
-            }
+            tix = find_tensor(tens, ntens, tix, chunk);
             const ga_demo_tensor td = tens[tix];
             const int c = chunk - td.chunk_start;
             int32_t* pi = payload0 + rep * pstride + td.payload_off + (int64_t)c * td.k;
@@ -697,7 +799,10 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
 #endif
             );
             DW_CNT(9);
-        } else {
+        }
+    }
+    for (; job < total; job += stride) {  // row groups
+        {
             const int64_t j = job - n64;
             const int64_t rep = j / ngroups;
             const int g = (int)(j - rep * ngroups);

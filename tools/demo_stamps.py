@@ -78,7 +78,7 @@ def main():
     st = stamps.view(-1, 16).cpu().numpy().astype(np.int64)
     if wave:  # one row per wave: 7 phase sums, [8] all-keys selections, [9] chunks
         st = st[st[:, 9] > 0]
-        tot = st[:, :8].sum(axis=1)
+        tot = st[:, :8].sum(axis=1) + st[:, 10:14].sum(axis=1)
         nch = st[:, 9]
         print(f"{model}: {plan.nchunks} chunks over {len(st)} waves, kernel {e0.elapsed_time(e1):.3f} ms "
               f"(stamped build); all-keys selections {st[:, 8].sum()} of {nch.sum()} chunks")
@@ -86,6 +86,11 @@ def main():
         for i, name in enumerate(WAVE_PHASES):
             v = st[:, i] / nch
             print(f"  {name:22s} median {np.median(v):8.0f} cyc/chunk  share {np.median(st[:, i] / tot):6.1%}")
+        for i, name in zip(range(10, 14), ["top-k: max/T0/count", "top-k: compaction", "top-k: bitmap ranks",
+                                           "top-k: k-th key+ties"]):
+            v = st[:, i] / nch
+            if v.any():
+                print(f"    {name:22s} median {np.median(v):8.0f} cyc/chunk  (part of the phases above)")
         return
     st = st[st[:, 8] > 0]  # workgroups that ran (persistent grid)
     tot = st[:, :6].sum(axis=1)
