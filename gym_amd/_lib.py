@@ -61,6 +61,8 @@ SIGNATURES = {
                                    c_f32, c_f32, c_f32, c_p, c_i64, c_i64, c_p]),
     "ga_demo_decode": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64,
                                c_i64, c_f32, c_p]),
+    "ga_demo_decode_sym": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p,
+                                   c_i64, c_i64, c_f32, c_p]),
     "ga_sumsq_partials_count": (c_i32, []),
     "ga_grad_clip_coef": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "ga_adam_step": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,

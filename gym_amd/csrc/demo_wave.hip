@@ -265,6 +265,44 @@ __device__ __forceinline__ void row_product(const float (&x)[2][8][4], const flo
     }
 }
 
+// ---- sparse synthesis R = sum_e v_e F[:, b_e] (x) F[:, d_e] in the row-pair layout ----
+// The entries (one per lane where `ent`) as per-parity-of-b lists lstp[par * 64 + i], an
+// odd list padded with a zero entry; np0 / np1 = entry pairs per list.
+__device__ __forceinline__ void parity_lists(uint32_t epos, uint32_t ebits, bool ent, int lane, uint2* lstp,
+                                             int& np0, int& np1) {
+    const int pl = (int)((epos >> 6) & 1u);
+    const uint64_t m0 = __ballot(ent && pl == 0), m1 = __ballot(ent && pl == 1);
+    const uint64_t mm = pl ? m1 : m0;
+    const int ix = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+    const int E0 = __popcll(m0), E1 = __popcll(m1);
+    WAVE_LDS_SYNC();
+    if (ent) lstp[pl * 64 + ix] = make_uint2(epos, ebits);
+    if (lane == 0 && (E0 & 1)) lstp[E0] = make_uint2(0u, 0u);  // odd count: a zero partner
+    if (lane == 1 && (E1 & 1)) lstp[64 + E1] = make_uint2(0u, 0u);
+    WAVE_LDS_SYNC();
+    np0 = (E0 + 1) >> 1;
+    np1 = (E1 + 1) >> 1;
+}
+
+// R^T of column half H per parity of b: lane (l, h) register 4qq + e holds the parity
+// sums for rows l (Re + Ro) and 63 - l (Re - Ro), column 4 blk(h, 4H + qq) + e
+__device__ __forceinline__ void synth_half(const uint2* lstp, int np0, int np1, int H, int l, int h,
+                                           const float* Hb, f32x16& Re, f32x16& Ro) {
+    const int cH = pi_col(H, l);
+    Re = zero16();
+    Ro = zero16();
+    for (int q = 0; q < np0; ++q) {  // lane half h takes entry 2q + h
+        const uint2 e = lstp[2 * q + h];
+        const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
+        Re = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Re);
+    }
+    for (int q = 0; q < np1; ++q) {
+        const uint2 e = lstp[64 + 2 * q + h];
+        const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
+        Ro = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Ro);
+    }
+}
+
 // ---- 64x64 chunk ------------------------------------------------------------
 // Global memory is read and written in the coalesced layout C -- lane t holds rows
 // (t >> 4) + 4i (i < 16), 4 elements at column 4 (t & 15): each access covers 4
@@ -597,36 +635,12 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
     //      column half H at a time
     uint2* lstp = reinterpret_cast<uint2*>(W.lst);  // [parity][64] entries
     int np0, np1;
-    {
-        const uint32_t epos = lane < k ? W.lst[2 * lane] : 0u;
-        const uint32_t ebits = lane < k ? W.lst[2 * lane + 1] : 0u;
-        const int pl = (int)((epos >> 6) & 1u);
-        const uint64_t m0 = __ballot(lane < k && pl == 0), m1 = __ballot(lane < k && pl == 1);
-        const uint64_t mm = pl ? m1 : m0;
-        const int ix = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
-        const int E0 = __popcll(m0), E1 = __popcll(m1);
-        WAVE_LDS_SYNC();
-        if (lane < k) lstp[pl * 64 + ix] = make_uint2(epos, ebits);
-        if (lane == 0 && (E0 & 1)) lstp[E0] = make_uint2(0u, 0u);  // odd count: a zero partner
-        if (lane == 1 && (E1 & 1)) lstp[64 + E1] = make_uint2(0u, 0u);
-        WAVE_LDS_SYNC();
-        np0 = (E0 + 1) >> 1;
-        np1 = (E1 + 1) >> 1;
-    }
+    parity_lists(lane < k ? W.lst[2 * lane] : 0u, lane < k ? W.lst[2 * lane + 1] : 0u, lane < k, lane, lstp, np0,
+                 np1);
 #pragma unroll
     for (int H = 0; H < 2; ++H) {
-        const int cH = pi_col(H, l);
-        f32x16 Re = zero16(), Ro = zero16();
-        for (int q = 0; q < np0; ++q) {  // lane half h takes entry 2q + h
-            const uint2 e = lstp[2 * q + h];
-            const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
-            Re = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Re);
-        }
-        for (int q = 0; q < np1; ++q) {
-            const uint2 e = lstp[64 + 2 * q + h];
-            const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
-            Ro = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Ro);
-        }
+        f32x16 Re, Ro;
+        synth_half(lstp, np0, np1, H, l, h, Hb, Re, Ro);
         // delta = x - R in the tile, at the lane's own blocks 4H .. 4H+3: row l gets
         // Re + Ro, row 63 - l gets Re - Ro
 #pragma unroll
@@ -843,6 +857,359 @@ static int launch(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, co
     return GA_OK;
 }
 
+// ============================================================================
+// Decode (ga_demo_decode_sym): the gathered payloads of S <= 15 sources,
+// scatter-mean per chunk (demo.py:331-352), inverse DCT, sign, and the SGD step
+// on every local replica (demo.py:192-209), one wavefront per chunk.
+//   S == 1   the entries' sparse synthesis (synth_half, as the encode residual)
+//   S >= 2   node-ordered scatter-add + 4-bit hit counts in LDS, the mean over
+//            hitters, then g = F . X . F^T as two folded 64-deep MFMA products:
+//            U = X . F^T (columns l and 63 - l from the even / odd-frequency
+//            halves), g^T = U^T . F^T (rows l and 63 - l from the even / odd b)
+// The signs go through the tile into the coalesced layout for the p update.
+// ============================================================================
+constexpr int kMaxSrc = 15;  // 4-bit hit counts
+
+struct DecLDS {
+    float tile[64 * 64];  // coefficients (swizzled row-major), then sign(g)
+    uint32_t aux[512];    // 4-bit hit counts per coefficient | the S == 1 parity lists
+};
+
+// float index of (row, col) in the swizzled tile (see t4)
+__device__ __forceinline__ int fidx(int row, int col) { return row * 64 + 4 * ((col >> 2) ^ (row & 15)) + (col & 3); }
+
+__device__ __forceinline__ float sgnf(float g) { return (float)((g > 0.f) - (g < 0.f)); }  // torch.sign, NaN -> 0
+
+// the signs (layout C, read from the tile where used) -> p -= lr * sign, grad = sign,
+// for each of K replicas; a full 64-row chunk's replica 0 comes in pre (loaded before
+// the chunk's transform, so the load latency hides behind it)
+template <typename T>
+__device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, int stride, bool vec, float lr,
+                                            int lane, float (&p)[16][4]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+        p[i][0] = fmaf(-lr, v.x, p[i][0]);
+        p[i][1] = fmaf(-lr, v.y, p[i][1]);
+        p[i][2] = fmaf(-lr, v.z, p[i][2]);
+        p[i][3] = fmaf(-lr, v.w, p[i][3]);
+    }
+    store_coal(pr, stride, vec, lane, p);
+    if (gr) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+            p[i][0] = v.x;
+            p[i][1] = v.y;
+            p[i][2] = v.z;
+            p[i][3] = v.w;
+        }
+        store_coal(gr, stride, vec, lane, p);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void apply_signs(const float4* tile, T* param, T* grad, int64_t K, int64_t ld, int stride,
+                                            bool vec, int nrows, float lr, int lane, float (&pre)[16][4]) {
+    if (nrows == 64) {
+        sign_update(tile, param, grad, stride, vec, lr, lane, pre);
+        for (int64_t r = 1; r < K; ++r) {
+            float p[16][4];
+            load_coal(param + r * ld, stride, vec, lane, p);
+            sign_update(tile, param + r * ld, grad ? grad + r * ld : nullptr, stride, vec, lr, lane, p);
+        }
+        return;
+    }
+    for (int64_t r = 0; r < K; ++r) {  // a partial row group
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if ((lane >> 4) + 4 * i >= nrows) continue;
+            const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+            const float sg[4] = {v.x, v.y, v.z, v.w};
+            T* a = at_off(param + r * ld, coal_off(i, lane, stride));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Elem<T>::store(a + e, fmaf(-lr, sg[e], Elem<T>::load(a + e)));
+            if (grad) {
+                T* gq = at_off(grad + r * ld, coal_off(i, lane, stride));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Elem<T>::store(gq + e, sg[e]);
+            }
+        }
+    }
+}
+
+// node-ordered scatter-add of S sources' entries (n per source, entry j -> tile row
+// row_of(j)) and the 4-bit hit counts; sources in order, one source per pass (a
+// source's indices are distinct, so the adds of one pass never collide)
+template <typename RowOf>
+__device__ __forceinline__ void scatter_sources(DecLDS& W, const int32_t* __restrict__ payload, int64_t pstride,
+                                                int64_t M, int64_t e0, int S, int n, int nvalid, RowOf row_of,
+                                                int lane) {
+    for (int s = 0; s < S; ++s) {
+        const int32_t* pi = payload + (int64_t)s * pstride + e0;
+        const float* pv = reinterpret_cast<const float*>(payload + (int64_t)s * pstride + M) + e0;
+        for (int j = lane; j < n; j += 64) {
+            const int x = pi[j];
+            const float v = pv[j];
+            if ((unsigned)x < (unsigned)nvalid) {
+                const int row = row_of(j, x), col = nvalid == 64 ? x : (x & 63);
+                atomicAdd(&W.tile[fidx(row, col)], v);
+                const int cid = row * 64 + col;
+                atomicAdd(&W.aux[cid >> 3], 1u << (4 * (cid & 7)));
+            }
+        }
+        WAVE_LDS_SYNC();
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void dchunk64(const ga_demo_tensor& td, int c, const int32_t* __restrict__ payload,
+                                         int64_t pstride, int64_t M, int S, T* param, T* grad, int64_t K, int64_t ld,
+                                         float lr, int ptr_vec, const float* Hb, DecLDS& W) {
+    const int k = td.k;
+    const int64_t e0 = td.payload_off + (int64_t)c * k;
+    const int cy = c / td.gx, cx = c - cy * td.gx;
+    const int64_t base = td.offset + (int64_t)cy * 64 * td.cols + (int64_t)cx * 64;
+    const bool vec = ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0);
+    float4* tile = reinterpret_cast<float4*>(W.tile);
+    const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+    // each source's entry `lane` (k <= 64), all loads in flight at once; replica 0's
+    // parameters are loaded once the entries are consumed, in flight behind the transform
+    float p0[16][4];
+    int xs[kMaxSrc];
+    float vs[kMaxSrc];
+#pragma unroll
+    for (int s = 0; s < kMaxSrc; ++s) {
+        xs[s] = -1;
+        vs[s] = 0.f;
+        if (s < S && lane < k) {
+            xs[s] = payload[(int64_t)s * pstride + e0 + lane];
+            vs[s] = reinterpret_cast<const float*>(payload + (int64_t)s * pstride + M)[e0 + lane];
+        }
+    }
+    if (S == 1) {
+        uint32_t epos = 0u, ebits = 0u;
+        bool ent = false;
+        if (lane < k) {
+            const int x = xs[0];
+            const float v = vs[0];
+            ent = (unsigned)x < 4096u;
+            epos = ent ? (uint32_t)x : 0u;
+            ebits = ent ? __float_as_uint(v) : 0u;
+        }
+        load_coal(param + base, td.cols, vec, lane, p0);
+        uint2* lstp = reinterpret_cast<uint2*>(W.aux);
+        int np0, np1;
+        parity_lists(epos, ebits, ent, lane, lstp, np0, np1);
+#pragma unroll
+        for (int H = 0; H < 2; ++H) {
+            f32x16 Re, Ro;
+            synth_half(lstp, np0, np1, H, l, h, Hb, Re, Ro);
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const int r = 4 * qq;
+                tile[t4(l, blk(h, 4 * H + qq))] = make_float4(sgnf(Re[r] + Ro[r]), sgnf(Re[r + 1] + Ro[r + 1]),
+                                                              sgnf(Re[r + 2] + Ro[r + 2]), sgnf(Re[r + 3] + Ro[r + 3]));
+                tile[t4(63 - l, blk(h, 4 * H + qq))] =
+                    make_float4(sgnf(Re[r] - Ro[r]), sgnf(Re[r + 1] - Ro[r + 1]), sgnf(Re[r + 2] - Ro[r + 2]),
+                                sgnf(Re[r + 3] - Ro[r + 3]));
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tile[i * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+        reinterpret_cast<uint4*>(W.aux)[lane] = make_uint4(0u, 0u, 0u, 0u);
+        reinterpret_cast<uint4*>(W.aux)[64 + lane] = make_uint4(0u, 0u, 0u, 0u);
+        WAVE_LDS_SYNC();
+        // node-ordered scatter-add with 4-bit hit counts, one source per pass (a
+        // source's indices are distinct: the adds of one pass never collide)
+#pragma unroll
+        for (int s = 0; s < kMaxSrc; ++s) {
+            const int x = xs[s];  // -1 past S
+            if ((unsigned)x < 4096u) {
+                atomicAdd(&W.tile[fidx(x >> 6, x & 63)], vs[s]);
+                atomicAdd(&W.aux[x >> 3], 1u << (4 * (x & 7)));
+            }
+            WAVE_LDS_SYNC();
+        }
+        // mean over the hitters (demo.py:331-352): every entry reads its coefficient's sum and
+        // count first, then entries of a coefficient hit more than once write the (same) mean
+        float mv[kMaxSrc];
+        int mi[kMaxSrc];
+#pragma unroll
+        for (int s = 0; s < kMaxSrc; ++s) {
+            mi[s] = -1;
+            mv[s] = 0.f;
+            const int x = xs[s];
+            if ((unsigned)x < 4096u) {
+                const int n = (int)((W.aux[x >> 3] >> (4 * (x & 7))) & 15u);
+                const int f = fidx(x >> 6, x & 63);
+                if (n > 1) {
+                    mi[s] = f;
+                    mv[s] = W.tile[f] / (float)n;
+                }
+            }
+        }
+        WAVE_LDS_SYNC();
+#pragma unroll
+        for (int s = 0; s < kMaxSrc; ++s)
+            if (mi[s] >= 0) W.tile[mi[s]] = mv[s];
+        WAVE_LDS_SYNC();
+        load_coal(param + base, td.cols, vec, lane, p0);
+        // U = X . F^T: U[b][l] = ue + uo, U[b][63 - l] = ue - uo (even / odd frequency d)
+        f32x16 U[2][2];  // [b block][column set]
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            f32x16 ue = zero16(), uo = zero16();
+            const int row = 32 * bb + l;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {  // lane half h: frequencies 32h + 4t .. +3
+                const float4 xv = tile[t4(row, 8 * h + t)];
+                const float* fr = Hb + l * kLd + 32 * h + 4 * t;
+                ue = mfma(xv.x, fr[0], ue);
+                uo = mfma(xv.y, fr[1], uo);
+                ue = mfma(xv.z, fr[2], ue);
+                uo = mfma(xv.w, fr[3], uo);
+            }
+            U[bb][0] = ue + uo;
+            U[bb][1] = ue - uo;
+        }
+        WAVE_LDS_SYNC();
+        // g^T = U^T . F^T per column set: row l gets ge + go, row 63 - l gets ge - go
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs) {
+            f32x16 ge = zero16(), go = zero16();
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int bb = s >> 3, r2 = 2 * (s & 7);
+                ge = mfma(U[bb][cs][r2], Hb[l * kLd + 32 * bb + rowmap(r2, h)], ge);
+                go = mfma(U[bb][cs][r2 + 1], Hb[l * kLd + 32 * bb + rowmap(r2 + 1, h)], go);
+            }
+            // register 4q' + e: column m = 8q' + 4h + e (cs = 0) or 63 - m (cs = 1)
+#pragma unroll
+            for (int qp = 0; qp < 4; ++qp) {
+                float a[4], b[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    a[e] = sgnf(ge[4 * qp + e] + go[4 * qp + e]);
+                    b[e] = sgnf(ge[4 * qp + e] - go[4 * qp + e]);
+                }
+                const int cb = cs ? 15 - (2 * qp + h) : 2 * qp + h;
+                tile[t4(l, cb)] = cs ? make_float4(a[3], a[2], a[1], a[0]) : make_float4(a[0], a[1], a[2], a[3]);
+                tile[t4(63 - l, cb)] = cs ? make_float4(b[3], b[2], b[1], b[0]) : make_float4(b[0], b[1], b[2], b[3]);
+            }
+        }
+    }
+    WAVE_LDS_SYNC();
+    apply_signs(tile, param + base, grad ? grad + base : nullptr, K, ld, td.cols, vec, 64, lr, lane, p0);
+    WAVE_LDS_SYNC();
+}
+
+// row group: rows = consecutive 1x64 chunks (contiguous, stride 64); g[row] = X[row] . F^T
+template <typename T>
+__device__ __forceinline__ void dgroup(const ga_demo_rowgroup& rg, const int32_t* __restrict__ payload,
+                                       int64_t pstride, int64_t M, int S, T* param, T* grad, int64_t K, int64_t ld,
+                                       float lr, int ptr_vec, const float* Hb, DecLDS& W) {
+    const int rows = rg.rows, k = rg.k;
+    const bool vec = ptr_vec && (rg.offset % 4 == 0);
+    float4* tile = reinterpret_cast<float4*>(W.tile);
+    const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+    float pre[16][4];  // a full group's replica 0, in flight behind the transform
+    if (rows == 64) load_coal(param + rg.offset, 64, vec, lane, pre);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tile[i * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    reinterpret_cast<uint4*>(W.aux)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(W.aux)[64 + lane] = make_uint4(0u, 0u, 0u, 0u);
+    WAVE_LDS_SYNC();
+    scatter_sources(W, payload, pstride, M, rg.payload_off, S, rows * k, 64, [k](int j, int) { return j / k; }, lane);
+    if (S > 1) {  // mean over the hitters: a pass over the whole tile (row groups are few)
+#pragma unroll 4
+        for (int i = 0; i < 64; ++i) {
+            const int cid = i * 64 + lane;
+            const int n = (int)((W.aux[cid >> 3] >> (4 * (cid & 7))) & 15u);
+            if (n > 1) W.tile[fidx(i, lane)] /= (float)n;
+        }
+        WAVE_LDS_SYNC();
+    }
+    // R^T[c][row] = sum_d F[c][d] X[row][d] for rows l (s = 0) and 63 - l (s = 1)
+    const int c0 = pi_col(0, l), c1 = pi_col(1, l);
+    f32x16 r[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int row = s ? 63 - l : l;
+        r[s][0] = zero16();
+        r[s][1] = zero16();
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int d = 2 * t + h;
+            const float xv = W.tile[fidx(row, d)];
+            r[s][0] = mfma(basis64(Hb, c0, d), xv, r[s][0]);
+            r[s][1] = mfma(basis64(Hb, c1, d), xv, r[s][1]);
+        }
+    }
+    WAVE_LDS_SYNC();
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const f32x16& a = r[s][q >> 2];
+            const int o = 4 * (q & 3);
+            tile[t4(s ? 63 - l : l, blk(h, q))] =
+                make_float4(sgnf(a[o]), sgnf(a[o + 1]), sgnf(a[o + 2]), sgnf(a[o + 3]));
+        }
+    WAVE_LDS_SYNC();
+    apply_signs(tile, param + rg.offset, grad ? grad + rg.offset : nullptr, K, ld, 64, vec, rows, lr, lane, pre);
+    WAVE_LDS_SYNC();
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void decode_kernel(
+    const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const ga_demo_rowgroup* __restrict__ groups,
+    int ngroups, const float* __restrict__ F64, const int32_t* __restrict__ payload, int64_t pstride, int64_t M,
+    int S, T* param, T* grad, int64_t K, int64_t ld, float lr, int ptr_vec) {
+    __shared__ float Hb[32 * kLd];
+    __shared__ DecLDS wl[kWaves];
+    for (int q = threadIdx.x; q < 32 * 64; q += kThreads) Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    DecLDS& W = wl[wid];
+    const int64_t total = (int64_t)nchunks + ngroups;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int tix = -1;
+    int64_t job = (int64_t)blockIdx.x * kWaves + wid;
+    for (; job < nchunks; job += stride) {
+        const int chunk = (int)job;
+        tix = find_tensor(tens, ntens, tix, chunk);
+        const ga_demo_tensor td = tens[tix];
+        dchunk64<T>(td, chunk - td.chunk_start, payload, pstride, M, S, param, grad, K, ld, lr, ptr_vec, Hb, W);
+    }
+    for (; job < total; job += stride) {
+        const ga_demo_rowgroup rg = groups[(int)(job - nchunks)];
+        dgroup<T>(rg, payload, pstride, M, S, param, grad, K, ld, lr, ptr_vec, Hb, W);
+    }
+}
+
+template <typename T>
+static void launch_decode(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, const ga_demo_rowgroup* groups,
+                          int32_t ngroups, const float* F64, const int32_t* payload, int64_t pstride, int64_t M,
+                          int S, void* param, void* grad, int64_t K, int64_t ld, float lr, int ptr_vec,
+                          hipStream_t stream) {
+    auto kern = decode_kernel<T>;
+    static const int resident = [&] {
+        int per_cu = 0, dev = 0, cus = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
+    }();
+    const int64_t jobs = (int64_t)nchunks + ngroups;
+    const int64_t want = (jobs + kWaves - 1) / kWaves;
+    const int grid = (int)(want < resident ? want : resident);
+    if (grid <= 0) return;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks, groups, ngroups, F64,
+                       payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
+}
+
 #ifdef GA_DEMO_STAMPS
 __device__ unsigned long long* g_demo_stamps_w;
 #endif
@@ -887,4 +1254,36 @@ extern "C" GA_API int ga_demo_encode_sym(int dtype, const ga_demo_tensor* tensor
         default: set_error("ga_demo_encode_sym: unknown dtype %d", dtype); return GA_EINVAL;
     }
     return check_launch("ga_demo_encode_sym");
+}
+
+extern "C" GA_API int ga_demo_decode_sym(int dtype, const ga_demo_tensor* tensors, int32_t ntensors,
+                                         int32_t nchunks, const ga_demo_rowgroup* groups, int32_t ngroups,
+                                         const float* F64, const int32_t* payload, int64_t payload_stride, int64_t M,
+                                         int64_t S, void* param, void* grad, int64_t K, int64_t ld, float lr,
+                                         hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(ntensors >= 0 && nchunks >= 0 && ngroups >= 0 && (nchunks > 0 || ngroups > 0),
+               "ga_demo_decode_sym: empty plan (ntensors=%d nchunks=%d ngroups=%d)", ntensors, nchunks, ngroups);
+    GA_REQUIRE(nchunks == 0 || (tensors && ntensors >= 1), "ga_demo_decode_sym: no descriptors");
+    GA_REQUIRE(ngroups == 0 || groups, "ga_demo_decode_sym: no row groups");
+    GA_REQUIRE(F64 && payload && param, "ga_demo_decode_sym: null buffer");
+    GA_REQUIRE(S >= 1 && S <= dw::kMaxSrc, "ga_demo_decode_sym: S=%lld sources (1..%d; use ga_demo_decode)",
+               (long long)S, dw::kMaxSrc);
+    GA_REQUIRE(S == 1 || payload_stride >= 2 * M, "ga_demo_decode_sym: payload_stride < 2*M");
+    GA_REQUIRE(K >= 1 && (K == 1 || ld > 0), "ga_demo_decode_sym: bad K=%lld / ld", (long long)K);
+    const int vb = dtype == GA_F32 ? 16 : 8;
+    const int ptr_vec = ((uintptr_t)param % vb == 0) && (grad == nullptr || (uintptr_t)grad % vb == 0) &&
+                        (K == 1 || ld % 4 == 0);
+    switch (dtype) {
+        case GA_F32:
+            dw::launch_decode<float>(tensors, ntensors, nchunks, groups, ngroups, F64, payload, payload_stride, M,
+                                     (int)S, param, grad, K, ld, lr, ptr_vec, stream);
+            break;
+        case GA_BF16:
+            dw::launch_decode<__hip_bfloat16>(tensors, ntensors, nchunks, groups, ngroups, F64, payload,
+                                              payload_stride, M, (int)S, param, grad, K, ld, lr, ptr_vec, stream);
+            break;
+        default: set_error("ga_demo_decode_sym: unknown dtype %d", dtype); return GA_EINVAL;
+    }
+    return check_launch("ga_demo_decode_sym");
 }

@@ -182,6 +182,9 @@ def demo_encode(plan, param, grad, delta, payload, lr, decay, wd_factor):
                                pl2.stride(0), plan.M, _stream()), "ga_demo_encode")
 
 
+DECODE_SYM_MAX_SOURCES = 15
+
+
 def demo_decode(plan, gathered, param, grad, lr):
     """gathered: int32 [S, >= 2*M] payloads of every node in node order;
     param/grad: [K, ld] replica sets (grad may be None)."""
@@ -198,6 +201,13 @@ def demo_decode(plan, gathered, param, grad, lr):
         raise ValueError("demo_decode: arena shorter than the plan")
     plan.to(p2.device)
     S = ga.shape[0]
+    # the wave-per-chunk decode for the same plans as the wave encode and S <= 15
+    # sources (4-bit hit counts); GA_DEMO_DECODE=block forces the block kernel
+    if plan.wave_encode and S <= DECODE_SYM_MAX_SOURCES and os.environ.get("GA_DEMO_DECODE") != "block":
+        check(lib().ga_demo_decode_sym(_dtype_code(p2), _p(plan.desc64), plan.n64tensors, plan.n64chunks,
+                                       _p(plan.groups), plan.ngroups, _p(plan.F64), _p(ga), ga.stride(0), plan.M, S,
+                                       _p(p2), _p(g2), K, ld, float(lr), _stream()), "ga_demo_decode_sym")
+        return
     check(lib().ga_demo_decode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.B), _p(ga),
                                ga.stride(0), plan.M, S, _p(p2), _p(g2), K, ld, float(lr), _stream()),
           "ga_demo_decode")

@@ -231,6 +231,21 @@ GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, int32_t nten
                           void* grad, int64_t K, int64_t ld, float lr,
                           hipStream_t stream);
 
+/*
+ * ga_demo_decode for the plans ga_demo_encode_sym takes (64x64 chunks in
+ * `tensors`, 1x64 chunks in `groups`, F64 the 64-point basis) and S <= 15
+ * sources: same arithmetic and replica update as ga_demo_decode
+ * (demo.py:192-209, 331-352), one wavefront per chunk or row group.  S == 1 is
+ * a sparse synthesis of the k entries; S >= 2 scatter-adds the sources in node
+ * order into an LDS tile with 4-bit hit counts, takes the mean over hitters and
+ * runs the inverse transform as two folded 64-deep MFMA products.
+ */
+GA_API int ga_demo_decode_sym(int dtype, const ga_demo_tensor* tensors, int32_t ntensors,
+                              int32_t nchunks, const ga_demo_rowgroup* groups, int32_t ngroups,
+                              const float* F64, const int32_t* payload, int64_t payload_stride,
+                              int64_t M, int64_t S, void* param, void* grad, int64_t K, int64_t ld,
+                              float lr, hipStream_t stream);
+
 /* ---- inner optimizer on the arena --------------------------------------- */
 
 /* Number of fp32 partials ga_grad_clip_coef needs in its `partials` buffer. */

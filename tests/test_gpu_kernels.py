@@ -517,3 +517,54 @@ def test_replica_mean_edge_sizes():
     out = torch.empty(3, device=DEV)
     ops.replica_mean(x, out)
     assert host(out).tolist() == [1.5, 2.5, 3.5]
+
+
+@pytest.mark.parametrize("S,kernel", [(1, "wave"), (2, "wave"), (3, "wave"), (8, "wave"), (15, "wave"), (16, "wave"),
+                                      (8, "block")])
+def test_demo_decode_sources_with_collisions(monkeypatch, S, kernel):
+    """Decode of S hand-made payloads whose entries collide heavily (every chunk
+    draws its k indices from a pool of 40-48 coefficients): scatter-mean over the
+    hitters, inverse DCT, sign, p -= lr*sign on 2 replicas, vs the oracle.  S <= 15
+    takes ga_demo_decode_sym (S = 16 falls back to ga_demo_decode)."""
+    from gym_amd import ops
+    if kernel == "block":
+        monkeypatch.setenv("GA_DEMO_DECODE", "block")
+    L, plan, a = _demo_setup(DEMO_WAVE_SHAPES, 2, seed=100 + S)
+    assert plan.wave_encode
+    rng = np.random.default_rng(S)
+    lr = 0.01
+    idx = np.zeros((S, plan.M), np.int32)
+    val = np.zeros((S, plan.M), np.float32)
+    e0 = 0
+    per_tensor = []
+    for shape in L.shapes:
+        R, C, n1, n2 = odemo.tensor_view(shape, 64)
+        kk = max(1, min(32, n1 * n2))
+        gy, gx = R // n1, C // n2
+        pool = min(n1 * n2, 40 if n1 > 1 else 48)
+        ti = np.sort(np.stack([np.stack([rng.choice(pool, kk, replace=False) for _ in range(gy * gx)])
+                               for _ in range(S)]), axis=-1).astype(np.int32)
+        tv = rng.standard_normal(ti.shape).astype(np.float32)
+        idx[:, e0:e0 + gy * gx * kk] = ti.reshape(S, -1)
+        val[:, e0:e0 + gy * gx * kk] = tv.reshape(S, -1)
+        per_tensor.append((ti.reshape(S, gy, gx, kk), tv.reshape(S, gy, gx, kk)))
+        e0 += gy * gx * kk
+    payload = torch.from_numpy(np.concatenate([idx, val.view(np.int32)], axis=1)).to(DEV)
+    P = t(a["p"])
+    Gs = torch.full_like(P, 7.0)
+    ops.demo_decode(plan, payload, P, Gs, lr)
+    gP, gS = host(P), host(Gs)
+    for (shape, off, nel), (ti, tv) in zip(zip(L.shapes, L.offsets, L.numels), per_tensor):
+        R, C, n1, n2 = odemo.tensor_view(shape, 64)
+        Y = odemo.scatter_mean(list(ti), list(tv), n1, n2)
+        g = odemo.decode(Y, shape, 64)
+        want_s = np.sign(g).astype(np.float32)
+        firm = np.abs(g) > 1e-5 * np.abs(g).max()
+        p0 = a["p"][0, off:off + nel].reshape(shape)
+        for k in range(2):
+            s = gS[k, off:off + nel].reshape(shape)
+            assert np.array_equal(s[firm], want_s[firm]), (shape, k)
+            assert np.isin(s, (-1.0, 0.0, 1.0)).all()
+            np.testing.assert_allclose(gP[k, off:off + nel].reshape(shape), p0 - lr * s, rtol=0, atol=1e-7)
+    for o, nel, o2 in zip(L.offsets, L.numels, L.offsets[1:] + [L.n]):  # padding untouched
+        assert (gS[:, o + nel:o2] == 7.0).all()
