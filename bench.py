@@ -271,10 +271,24 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
     t8.on = True
     timed_loop(dec8, args.steps, args.warmup, coll)
     dec8_ms = t8.mean_ms()
+    tn = KernelTimer()  # the same decode without the grad write (p only)
+    decn = tn.wrap(lambda: ops.demo_decode(plan, codec.payload[0:1], P, None, 1e-3))
+    tn.on = True
+    timed_loop(decn, args.steps, args.warmup, coll)
+    n = numel(shapes)
+    # algorithmic HBM bytes: encode reads delta, g and writes delta (wd = 0) + the
+    # payload; decode reads p, writes p and grad + S payloads (8 B per entry)
+    enc_bytes = 12 * n + 8 * plan.M
+    dec_bytes = 12 * n + 8 * plan.M
     return {"ms_per_step": round(t * 1e3, 4), "model": model, "nodes": coll.world,
             "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4), "decode_8src_ms": round(dec8_ms, 4),
-            "encode_TFLOPs": round(2 * flops_one / (enc_ms * 1e-3) / 1e12, 2),
-            "decode_TFLOPs": round(flops_one / (dec_ms * 1e-3) / 1e12, 2),
+            "decode_nograd_ms": round(tn.mean_ms(), 4),
+            "encode_HBM_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
+            "decode_HBM_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
+            "decode_8src_HBM_GBps": round((dec_bytes + 7 * 8 * plan.M) / (dec8_ms * 1e-3) / 1e9, 1),
+            # dense-formulation flops of SURVEY 8(d); the folded kernels issue half of them
+            "encode_dense_TFLOPs": round(2 * flops_one / (enc_ms * 1e-3) / 1e12, 2),
+            "decode_dense_TFLOPs": round(flops_one / (dec_ms * 1e-3) / 1e12, 2),
             "mfma_f32_peak_TFLOPs": MFMA_F32_TFLOPS, "payload_entries": plan.M,
             "ref_bytes_tx": plan.reference_bytes()}
 

@@ -962,31 +962,56 @@ __device__ __forceinline__ void scatter_sources(DecLDS& W, const int32_t* __rest
     }
 }
 
-template <typename T>
-__device__ __forceinline__ void dchunk64(const ga_demo_tensor& td, int c, const int32_t* __restrict__ payload,
-                                         int64_t pstride, int64_t M, int S, T* param, T* grad, int64_t K, int64_t ld,
-                                         float lr, int ptr_vec, const float* Hb, DecLDS& W) {
-    const int k = td.k;
-    const int64_t e0 = td.payload_off + (int64_t)c * k;
-    const int cy = c / td.gx, cx = c - cy * td.gx;
-    const int64_t base = td.offset + (int64_t)cy * 64 * td.cols + (int64_t)cx * 64;
-    const bool vec = ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0);
-    float4* tile = reinterpret_cast<float4*>(W.tile);
-    const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-    // each source's entry `lane` (k <= 64), all loads in flight at once; replica 0's
-    // parameters are loaded once the entries are consumed, in flight behind the transform
-    float p0[16][4];
+// sum / (hit count in the low nibble of cw), true division as scatter_reduce_(mean)
+__device__ __forceinline__ float mean_of(float sum, uint32_t cw) {
+    const uint32_t n = cw & 15u;
+    return n > 1u ? sum / (float)n : sum;
+}
+
+// a 64x64 chunk's global inputs: each source's entry `lane` (k <= 64) and replica 0's
+// parameters (layout C)
+struct DecIn {
     int xs[kMaxSrc];
     float vs[kMaxSrc];
+};
+
+__device__ __forceinline__ int64_t chunk_base(const ga_demo_tensor& td, int c) {
+    const int cy = c / td.gx, cx = c - cy * td.gx;
+    return td.offset + (int64_t)cy * 64 * td.cols + (int64_t)cx * 64;
+}
+
+__device__ __forceinline__ bool chunk_vec(const ga_demo_tensor& td, int ptr_vec) {
+    return ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0);
+}
+
+// issue the loads of chunk c's entries, all sources at once
+__device__ __forceinline__ void dchunk_entries(const ga_demo_tensor& td, int c, const int32_t* __restrict__ payload,
+                                               int64_t pstride, int64_t M, int S, DecIn& in) {
+    const int k = td.k, lane = lane_id();
+    const int64_t e0 = td.payload_off + (int64_t)c * k;
 #pragma unroll
     for (int s = 0; s < kMaxSrc; ++s) {
-        xs[s] = -1;
-        vs[s] = 0.f;
+        in.xs[s] = -1;
+        in.vs[s] = 0.f;
         if (s < S && lane < k) {
-            xs[s] = payload[(int64_t)s * pstride + e0 + lane];
-            vs[s] = reinterpret_cast<const float*>(payload + (int64_t)s * pstride + M)[e0 + lane];
+            in.xs[s] = payload[(int64_t)s * pstride + e0 + lane];
+            in.vs[s] = reinterpret_cast<const float*>(payload + (int64_t)s * pstride + M)[e0 + lane];
         }
     }
+}
+
+template <typename T>
+__device__ __forceinline__ void dchunk_params(const ga_demo_tensor& td, int c, const T* param, int ptr_vec,
+                                              float (&p0)[16][4]) {
+    load_coal(param + chunk_base(td, c), td.cols, chunk_vec(td, ptr_vec), lane_id(), p0);
+}
+
+// sign(g) of chunk c into the tile (swizzled row-major) from the entries in `in`
+__device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn& in, const float* Hb, DecLDS& W) {
+    float4* tile = reinterpret_cast<float4*>(W.tile);
+    const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+    const int (&xs)[kMaxSrc] = in.xs;
+    const float (&vs)[kMaxSrc] = in.vs;
     if (S == 1) {
         uint32_t epos = 0u, ebits = 0u;
         bool ent = false;
@@ -997,7 +1022,6 @@ __device__ __forceinline__ void dchunk64(const ga_demo_tensor& td, int c, const 
             epos = ent ? (uint32_t)x : 0u;
             ebits = ent ? __float_as_uint(v) : 0u;
         }
-        load_coal(param + base, td.cols, vec, lane, p0);
         uint2* lstp = reinterpret_cast<uint2*>(W.aux);
         int np0, np1;
         parity_lists(epos, ebits, ent, lane, lstp, np0, np1);
@@ -1032,30 +1056,6 @@ __device__ __forceinline__ void dchunk64(const ga_demo_tensor& td, int c, const 
             }
             WAVE_LDS_SYNC();
         }
-        // mean over the hitters (demo.py:331-352): every entry reads its coefficient's sum and
-        // count first, then entries of a coefficient hit more than once write the (same) mean
-        float mv[kMaxSrc];
-        int mi[kMaxSrc];
-#pragma unroll
-        for (int s = 0; s < kMaxSrc; ++s) {
-            mi[s] = -1;
-            mv[s] = 0.f;
-            const int x = xs[s];
-            if ((unsigned)x < 4096u) {
-                const int n = (int)((W.aux[x >> 3] >> (4 * (x & 7))) & 15u);
-                const int f = fidx(x >> 6, x & 63);
-                if (n > 1) {
-                    mi[s] = f;
-                    mv[s] = W.tile[f] / (float)n;
-                }
-            }
-        }
-        WAVE_LDS_SYNC();
-#pragma unroll
-        for (int s = 0; s < kMaxSrc; ++s)
-            if (mi[s] >= 0) W.tile[mi[s]] = mv[s];
-        WAVE_LDS_SYNC();
-        load_coal(param + base, td.cols, vec, lane, p0);
         // U = X . F^T: U[b][l] = ue + uo, U[b][63 - l] = ue - uo (even / odd frequency d)
         f32x16 U[2][2];  // [b block][column set]
 #pragma unroll
@@ -1064,7 +1064,13 @@ __device__ __forceinline__ void dchunk64(const ga_demo_tensor& td, int c, const 
             const int row = 32 * bb + l;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {  // lane half h: frequencies 32h + 4t .. +3
-                const float4 xv = tile[t4(row, 8 * h + t)];
+                // the mean over the hitters (demo.py:331-352), applied as the sums are read
+                float4 xv = tile[t4(row, 8 * h + t)];
+                const uint32_t cw = W.aux[(row * 64 + 32 * h + 4 * t) >> 3] >> (16 * (t & 1));
+                xv.x = mean_of(xv.x, cw);
+                xv.y = mean_of(xv.y, cw >> 4);
+                xv.z = mean_of(xv.z, cw >> 8);
+                xv.w = mean_of(xv.w, cw >> 12);
                 const float* fr = Hb + l * kLd + 32 * h + 4 * t;
                 ue = mfma(xv.x, fr[0], ue);
                 uo = mfma(xv.y, fr[1], uo);
@@ -1100,8 +1106,6 @@ __device__ __forceinline__ void dchunk64(const ga_demo_tensor& td, int c, const 
             }
         }
     }
-    WAVE_LDS_SYNC();
-    apply_signs(tile, param + base, grad ? grad + base : nullptr, K, ld, td.cols, vec, 64, lr, lane, p0);
     WAVE_LDS_SYNC();
 }
 
@@ -1177,11 +1181,34 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int tix = -1;
     int64_t job = (int64_t)blockIdx.x * kWaves + wid;
-    for (; job < nchunks; job += stride) {
-        const int chunk = (int)job;
-        tix = find_tensor(tens, ntens, tix, chunk);
-        const ga_demo_tensor td = tens[tix];
-        dchunk64<T>(td, chunk - td.chunk_start, payload, pstride, M, S, param, grad, K, ld, lr, ptr_vec, Hb, W);
+    // 64x64 chunks, software-pipelined: chunk j+1's entries are loaded before chunk j's
+    // stores (vmcnt retires in order: a load issued behind the stores would wait for
+    // them) and its parameters right after them, a whole transform ahead of their use
+    if (job < nchunks) {
+        DecIn cur;
+        float p0[16][4];
+        tix = find_tensor(tens, ntens, tix, (int)job);
+        ga_demo_tensor td = tens[tix];
+        dchunk_entries(td, (int)job - td.chunk_start, payload, pstride, M, S, cur);
+        dchunk_params<T>(td, (int)job - td.chunk_start, param, ptr_vec, p0);
+        while (true) {
+            const int c = (int)job - td.chunk_start;
+            dchunk_signs(td.k, S, cur, Hb, W);
+            const int64_t base = chunk_base(td, c);
+            const bool vec = chunk_vec(td, ptr_vec);
+            const int cols = td.cols;
+            job += stride;
+            if (job < nchunks) {
+                tix = find_tensor(tens, ntens, tix, (int)job);
+                td = tens[tix];
+                dchunk_entries(td, (int)job - td.chunk_start, payload, pstride, M, S, cur);
+            }
+            apply_signs(reinterpret_cast<const float4*>(W.tile), param + base, grad ? grad + base : nullptr, K, ld,
+                        cols, vec, 64, lr, lane_id(), p0);
+            WAVE_LDS_SYNC();
+            if (job >= nchunks) break;
+            dchunk_params<T>(td, (int)job - td.chunk_start, param, ptr_vec, p0);
+        }
     }
     for (; job < total; job += stride) {
         const ga_demo_rowgroup rg = groups[(int)(job - nchunks)];
