@@ -266,8 +266,10 @@ __device__ __forceinline__ void row_product(const float (&x)[2][8][4], const flo
 }
 
 // ---- sparse synthesis R = sum_e v_e F[:, b_e] (x) F[:, d_e] in the row-pair layout ----
-// The entries (one per lane where `ent`) as per-parity-of-b lists lstp[par * 64 + i], an
-// odd list padded with a zero entry; np0 / np1 = entry pairs per list.
+// The entries (one per lane where `ent`) as per-parity-of-b lists lstp[par * 64 + i], each
+// padded with zero entries to a multiple of kSynB pairs; np0 / np1 = entry pairs per list.
+constexpr int kSynB = 4;  // entry pairs per synthesis batch (LDS reads issued ahead of the MFMAs)
+
 __device__ __forceinline__ void parity_lists(uint32_t epos, uint32_t ebits, bool ent, int lane, uint2* lstp,
                                              int& np0, int& np1) {
     const int pl = (int)((epos >> 6) & 1u);
@@ -275,13 +277,35 @@ __device__ __forceinline__ void parity_lists(uint32_t epos, uint32_t ebits, bool
     const uint64_t mm = pl ? m1 : m0;
     const int ix = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
     const int E0 = __popcll(m0), E1 = __popcll(m1);
+    constexpr int kPad = 2 * kSynB;
+    const int P0 = (E0 + kPad - 1) / kPad * kPad, P1 = (E1 + kPad - 1) / kPad * kPad;  // <= 64
     WAVE_LDS_SYNC();
     if (ent) lstp[pl * 64 + ix] = make_uint2(epos, ebits);
-    if (lane == 0 && (E0 & 1)) lstp[E0] = make_uint2(0u, 0u);  // odd count: a zero partner
-    if (lane == 1 && (E1 & 1)) lstp[64 + E1] = make_uint2(0u, 0u);
+    if (lane < kPad && E0 + lane < P0) lstp[E0 + lane] = make_uint2(0u, 0u);  // zero partners
+    if (lane < kPad && E1 + lane < P1) lstp[64 + E1 + lane] = make_uint2(0u, 0u);
     WAVE_LDS_SYNC();
-    np0 = (E0 + 1) >> 1;
-    np1 = (E1 + 1) >> 1;
+    np0 = P0 >> 1;
+    np1 = P1 >> 1;
+}
+
+// one parity list's sum into acc, kSynB pairs per batch: the batch's entry and basis
+// reads go out together, then its MFMAs (lane half h takes entry 2q + h)
+__device__ __forceinline__ void synth_list(const uint2* lst, int np, int cH, int l, int h, const float* Hb,
+                                           f32x16& acc) {
+    for (int q = 0; q < np; q += kSynB) {
+        uint2 e[kSynB];
+#pragma unroll
+        for (int u = 0; u < kSynB; ++u) e[u] = lst[2 * (q + u) + h];
+        float a[kSynB], b[kSynB];
+#pragma unroll
+        for (int u = 0; u < kSynB; ++u) {
+            const int bq = (int)(e[u].x >> 6), dq = (int)(e[u].x & 63);
+            a[u] = __uint_as_float(e[u].y) * basis64(Hb, cH, dq);
+            b[u] = Hb[l * kLd + bq];
+        }
+#pragma unroll
+        for (int u = 0; u < kSynB; ++u) acc = mfma(a[u], b[u], acc);
+    }
 }
 
 // R^T of column half H per parity of b: lane (l, h) register 4qq + e holds the parity
@@ -291,16 +315,8 @@ __device__ __forceinline__ void synth_half(const uint2* lstp, int np0, int np1, 
     const int cH = pi_col(H, l);
     Re = zero16();
     Ro = zero16();
-    for (int q = 0; q < np0; ++q) {  // lane half h takes entry 2q + h
-        const uint2 e = lstp[2 * q + h];
-        const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
-        Re = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Re);
-    }
-    for (int q = 0; q < np1; ++q) {
-        const uint2 e = lstp[64 + 2 * q + h];
-        const int bq = (int)(e.x >> 6), dq = (int)(e.x & 63);
-        Ro = mfma(__uint_as_float(e.y) * basis64(Hb, cH, dq), Hb[l * kLd + bq], Ro);
-    }
+    synth_list(lstp, np0, cH, l, h, Hb, Re);
+    synth_list(lstp + 64, np1, cH, l, h, Hb, Ro);
 }
 
 // ---- 64x64 chunk ------------------------------------------------------------
