@@ -1,0 +1,115 @@
+// Random-word ceiling for SPARTA's access pattern on MI355X: M ~ p*N selected
+// positions (ascending) in each of K replicas of an N-element fp32 arena, read
+// and written back (4-B words at random 64-B sectors).  Standalone tool:
+//   hipcc -O3 --offload-arch=gfx950 tools/ubench_gather.hip -o build/ubench_gather
+// Orders: (a) element-major (lanes over replicas of one position), (b) replica-
+// major over the whole list, (c) tile-grouped (a workgroup per 4096-element tile,
+// replica-major inside it: what ga_sparta_average_local does, minus the mask).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <random>
+#include <vector>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+__global__ void rmw_elem_major(float* a, long ld, const int* pos, long M, int K) {
+    const long tot = M * K;
+    for (long f = (long)blockIdx.x * blockDim.x + threadIdx.x; f < tot; f += (long)gridDim.x * blockDim.x) {
+        const long j = f / K, k = f - j * K;
+        float* p = a + k * ld + pos[j];
+        *p = *p * 0.5f + 1.f;
+    }
+}
+
+__global__ void rmw_rep_major(float* a, long ld, const int* pos, long M, int K) {
+    const long tot = M * K;
+    for (long f = (long)blockIdx.x * blockDim.x + threadIdx.x; f < tot; f += (long)gridDim.x * blockDim.x) {
+        const long k = f / M, j = f - k * M;
+        float* p = a + k * ld + pos[j];
+        *p = *p * 0.5f + 1.f;
+    }
+}
+
+// one workgroup per tile: tile_start[t] .. tile_start[t+1] positions, replica-major
+__global__ __launch_bounds__(256) void rmw_tiles(float* a, long ld, const int* pos, const int* tile_start, int K) {
+    const int b = tile_start[blockIdx.x], e = tile_start[blockIdx.x + 1], c = e - b;
+    for (int f = threadIdx.x; f < c * K; f += 256) {
+        const int k = f / c, j = f - k * c;
+        float* p = a + (long)k * ld + pos[b + j];
+        *p = *p * 0.5f + 1.f;
+    }
+}
+
+// read-only variant of (c): per-position sums over the K replicas
+__global__ __launch_bounds__(256) void read_tiles(const float* a, long ld, const int* pos, const int* tile_start,
+                                                   int K, float* out) {
+    __shared__ float acc[512];
+    const int b = tile_start[blockIdx.x], e = tile_start[blockIdx.x + 1], c = e - b;
+    for (int f = threadIdx.x; f < 512; f += 256) acc[f] = 0.f;
+    __syncthreads();
+    for (int f = threadIdx.x; f < c * K; f += 256) {
+        const int k = f / c, j = f - k * c;
+        atomicAdd(&acc[j & 511], a[(long)k * ld + pos[b + j]]);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < c; j += 256) out[b + j] = acc[j & 511];
+}
+
+template <typename F>
+float time_ms(F f, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) f();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / reps;
+}
+
+int main() {
+    const int K = 32;
+    const long n = 124475904, ld = n;
+    const double p = 0.005;
+    std::mt19937_64 rng(42);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    std::vector<int> pos;
+    const long tiles = (n + 4095) / 4096;
+    std::vector<int> ts(tiles + 1, 0);
+    for (long i = 0; i < n; ++i) {
+        if (U(rng) < p) pos.push_back((int)i);
+        if ((i & 4095) == 4095 || i == n - 1) ts[i / 4096 + 1] = (int)pos.size();
+    }
+    const long M = (long)pos.size();
+    printf("n=%ld K=%d M=%ld pairs=%ld\n", n, K, M, M * K);
+    float *a, *out;
+    int *dpos, *dts;
+    CK(hipMalloc(&a, sizeof(float) * K * ld));
+    CK(hipMemset(a, 0, sizeof(float) * K * ld));
+    CK(hipMalloc(&out, sizeof(float) * M));
+    CK(hipMalloc(&dpos, sizeof(int) * M));
+    CK(hipMalloc(&dts, sizeof(int) * (tiles + 1)));
+    CK(hipMemcpy(dpos, pos.data(), sizeof(int) * M, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dts, ts.data(), sizeof(int) * (tiles + 1), hipMemcpyHostToDevice));
+    const int reps = 10;
+    const double pairs = (double)M * K;
+    auto rep = [&](const char* name, float ms, int rw) {
+        printf("%-28s %.3f ms  %.1f G words/s  %.0f GB/s at %d B per word\n", name, ms, pairs / ms / 1e6,
+               pairs * (rw ? 96 : 64) / ms / 1e6, rw ? 96 : 64);
+    };
+    for (int g : {4096, 16384, 65536}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "rmw element-major g=%d", g);
+        rep(nm, time_ms([&] { rmw_elem_major<<<g, 256>>>(a, ld, dpos, M, K); }, reps), 1);
+        snprintf(nm, sizeof nm, "rmw replica-major g=%d", g);
+        rep(nm, time_ms([&] { rmw_rep_major<<<g, 256>>>(a, ld, dpos, M, K); }, reps), 1);
+    }
+    rep("rmw tile-grouped", time_ms([&] { rmw_tiles<<<(unsigned)tiles, 256>>>(a, ld, dpos, dts, K); }, reps), 1);
+    rep("read tile-grouped", time_ms([&] { read_tiles<<<(unsigned)tiles, 256>>>(a, ld, dpos, dts, K, out); }, reps), 0);
+    CK(hipFree(a));
+    return 0;
+}
