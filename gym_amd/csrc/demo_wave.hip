@@ -267,7 +267,7 @@ __device__ __forceinline__ void row_product(const float (&x)[2][8][4], const flo
 
 // ---- sparse synthesis R = sum_e v_e F[:, b_e] (x) F[:, d_e] in the row-pair layout ----
 // The entries (one per lane where `ent`) as per-parity-of-b lists lstp[par * 64 + i], each
-// padded with zero entries to a multiple of kSynB pairs; np0 / np1 = entry pairs per list.
+// padded with a zero entry to whole pairs; np0 / np1 = entry pairs per list.
 constexpr int kSynB = 4;  // entry pairs per synthesis batch (LDS reads issued ahead of the MFMAs)
 
 __device__ __forceinline__ void parity_lists(uint32_t epos, uint32_t ebits, bool ent, int lane, uint2* lstp,
@@ -277,35 +277,47 @@ __device__ __forceinline__ void parity_lists(uint32_t epos, uint32_t ebits, bool
     const uint64_t mm = pl ? m1 : m0;
     const int ix = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
     const int E0 = __popcll(m0), E1 = __popcll(m1);
-    constexpr int kPad = 2 * kSynB;
-    const int P0 = (E0 + kPad - 1) / kPad * kPad, P1 = (E1 + kPad - 1) / kPad * kPad;  // <= 64
+    const int P0 = (E0 + 1) & ~1, P1 = (E1 + 1) & ~1;  // <= 64
     WAVE_LDS_SYNC();
     if (ent) lstp[pl * 64 + ix] = make_uint2(epos, ebits);
-    if (lane < kPad && E0 + lane < P0) lstp[E0 + lane] = make_uint2(0u, 0u);  // zero partners
-    if (lane < kPad && E1 + lane < P1) lstp[64 + E1 + lane] = make_uint2(0u, 0u);
+    if (lane == 0 && E0 < P0) lstp[E0] = make_uint2(0u, 0u);  // zero partners
+    if (lane == 1 && E1 < P1) lstp[64 + E1] = make_uint2(0u, 0u);
     WAVE_LDS_SYNC();
     np0 = P0 >> 1;
     np1 = P1 >> 1;
 }
 
-// one parity list's sum into acc, kSynB pairs per batch: the batch's entry and basis
-// reads go out together, then its MFMAs (lane half h takes entry 2q + h)
+// B pairs of one parity list into acc: the entry and basis reads go out together,
+// then the MFMAs (lane half h takes entry 2q + h)
+template <int B>
+__device__ __forceinline__ void synth_batch(const uint2* lst, int q, int cH, int l, int h, const float* Hb,
+                                            f32x16& acc) {
+    uint2 e[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) e[u] = lst[2 * (q + u) + h];
+    float a[B], b[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+        const int bq = (int)(e[u].x >> 6), dq = (int)(e[u].x & 63);
+        a[u] = __uint_as_float(e[u].y) * basis64(Hb, cH, dq);
+        b[u] = Hb[l * kLd + bq];
+    }
+#pragma unroll
+    for (int u = 0; u < B; ++u) acc = mfma(a[u], b[u], acc);
+}
+
+// one parity list's sum into acc: kSynB pairs per batch, then the 0..kSynB-1 left
+// (whole pairs only: no MFMA spent on padding beyond one zero entry)
 __device__ __forceinline__ void synth_list(const uint2* lst, int np, int cH, int l, int h, const float* Hb,
                                            f32x16& acc) {
-    for (int q = 0; q < np; q += kSynB) {
-        uint2 e[kSynB];
-#pragma unroll
-        for (int u = 0; u < kSynB; ++u) e[u] = lst[2 * (q + u) + h];
-        float a[kSynB], b[kSynB];
-#pragma unroll
-        for (int u = 0; u < kSynB; ++u) {
-            const int bq = (int)(e[u].x >> 6), dq = (int)(e[u].x & 63);
-            a[u] = __uint_as_float(e[u].y) * basis64(Hb, cH, dq);
-            b[u] = Hb[l * kLd + bq];
-        }
-#pragma unroll
-        for (int u = 0; u < kSynB; ++u) acc = mfma(a[u], b[u], acc);
+    int q = 0;
+    for (; q + kSynB <= np; q += kSynB) synth_batch<kSynB>(lst, q, cH, l, h, Hb, acc);
+    const int rem = np - q;
+    if (rem >= 2) {
+        synth_batch<2>(lst, q, cH, l, h, Hb, acc);
+        q += 2;
     }
+    if (rem & 1) synth_batch<1>(lst, q, cH, l, h, Hb, acc);
 }
 
 // R^T of column half H per parity of b: lane (l, h) register 4qq + e holds the parity
@@ -391,8 +403,12 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
             store_coal(param, td.cols, vec, lane, pv);
         }
         float Dv[16][4], Gv[16][4];
+        // the chunk's loads go out ahead of the partner wave's transforms (measured
+        // -0.7% on the 350M encode; the products themselves stay at priority 0)
+        __builtin_amdgcn_s_setprio(2);
         load_coal(delta, td.cols, vec, lane, Dv);
         load_coal(grad, td.cols, vec, lane, Gv);
+        __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             float v[4];
