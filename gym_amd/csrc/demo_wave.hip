@@ -1000,11 +1000,12 @@ __device__ __forceinline__ float mean_of(float sum, uint32_t cw) {
     return n > 1u ? sum / (float)n : sum;
 }
 
-// a 64x64 chunk's global inputs: each source's entry `lane` (k <= 64) and replica 0's
-// parameters (layout C)
+// a 64x64 chunk's global inputs: each source's entry `lane` (k <= 64), MS >= S register
+// slots (the kernel is built for MS = 8 and 15: at most 8 sources it holds no spill)
+template <int MS>
 struct DecIn {
-    int xs[kMaxSrc];
-    float vs[kMaxSrc];
+    int xs[MS];
+    float vs[MS];
 };
 
 __device__ __forceinline__ int64_t chunk_base(const ga_demo_tensor& td, int c) {
@@ -1017,12 +1018,13 @@ __device__ __forceinline__ bool chunk_vec(const ga_demo_tensor& td, int ptr_vec)
 }
 
 // issue the loads of chunk c's entries, all sources at once
+template <int MS>
 __device__ __forceinline__ void dchunk_entries(const ga_demo_tensor& td, int c, const int32_t* __restrict__ payload,
-                                               int64_t pstride, int64_t M, int S, DecIn& in) {
+                                               int64_t pstride, int64_t M, int S, DecIn<MS>& in) {
     const int k = td.k, lane = lane_id();
     const int64_t e0 = td.payload_off + (int64_t)c * k;
 #pragma unroll
-    for (int s = 0; s < kMaxSrc; ++s) {
+    for (int s = 0; s < MS; ++s) {
         in.xs[s] = -1;
         in.vs[s] = 0.f;
         if (s < S && lane < k) {
@@ -1039,11 +1041,12 @@ __device__ __forceinline__ void dchunk_params(const ga_demo_tensor& td, int c, c
 }
 
 // sign(g) of chunk c into the tile (swizzled row-major) from the entries in `in`
-__device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn& in, const float* Hb, DecLDS& W) {
+template <int MS>
+__device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn<MS>& in, const float* Hb, DecLDS& W) {
     float4* tile = reinterpret_cast<float4*>(W.tile);
     const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-    const int (&xs)[kMaxSrc] = in.xs;
-    const float (&vs)[kMaxSrc] = in.vs;
+    const int (&xs)[MS] = in.xs;
+    const float (&vs)[MS] = in.vs;
     if (S == 1) {
         uint32_t epos = 0u, ebits = 0u;
         bool ent = false;
@@ -1080,7 +1083,7 @@ __device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn& in, cons
         // node-ordered scatter-add with 4-bit hit counts, one source per pass (a
         // source's indices are distinct: the adds of one pass never collide)
 #pragma unroll
-        for (int s = 0; s < kMaxSrc; ++s) {
+        for (int s = 0; s < MS; ++s) {
             const int x = xs[s];  // -1 past S
             if ((unsigned)x < 4096u) {
                 atomicAdd(&W.tile[fidx(x >> 6, x & 63)], vs[s]);
@@ -1198,7 +1201,7 @@ __device__ __forceinline__ void dgroup(const ga_demo_rowgroup& rg, const int32_t
     WAVE_LDS_SYNC();
 }
 
-template <typename T>
+template <typename T, int MS>
 __global__ __launch_bounds__(kThreads) void decode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const ga_demo_rowgroup* __restrict__ groups,
     int ngroups, const float* __restrict__ F64, const int32_t* __restrict__ payload, int64_t pstride, int64_t M,
@@ -1217,7 +1220,7 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     // stores (vmcnt retires in order: a load issued behind the stores would wait for
     // them) and its parameters right after them, a whole transform ahead of their use
     if (job < nchunks) {
-        DecIn cur;
+        DecIn<MS> cur;
         float p0[16][4];
         tix = find_tensor(tens, ntens, tix, (int)job);
         ga_demo_tensor td = tens[tix];
@@ -1248,12 +1251,12 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     }
 }
 
-template <typename T>
-static void launch_decode(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, const ga_demo_rowgroup* groups,
-                          int32_t ngroups, const float* F64, const int32_t* payload, int64_t pstride, int64_t M,
-                          int S, void* param, void* grad, int64_t K, int64_t ld, float lr, int ptr_vec,
-                          hipStream_t stream) {
-    auto kern = decode_kernel<T>;
+template <typename T, int MS>
+static void launch_decode_ms(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks,
+                             const ga_demo_rowgroup* groups, int32_t ngroups, const float* F64,
+                             const int32_t* payload, int64_t pstride, int64_t M, int S, void* param, void* grad,
+                             int64_t K, int64_t ld, float lr, int ptr_vec, hipStream_t stream) {
+    auto kern = decode_kernel<T, MS>;
     static const int resident = [&] {
         int per_cu = 0, dev = 0, cus = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0);
@@ -1267,6 +1270,19 @@ static void launch_decode(const ga_demo_tensor* tens, int32_t ntens, int32_t nch
     if (grid <= 0) return;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks, groups, ngroups, F64,
                        payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
+}
+
+template <typename T>
+static void launch_decode(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, const ga_demo_rowgroup* groups,
+                          int32_t ngroups, const float* F64, const int32_t* payload, int64_t pstride, int64_t M,
+                          int S, void* param, void* grad, int64_t K, int64_t ld, float lr, int ptr_vec,
+                          hipStream_t stream) {
+    if (S <= 8)
+        launch_decode_ms<T, 8>(tens, ntens, nchunks, groups, ngroups, F64, payload, pstride, M, S, param, grad, K, ld,
+                               lr, ptr_vec, stream);
+    else
+        launch_decode_ms<T, kMaxSrc>(tens, ntens, nchunks, groups, ngroups, F64, payload, pstride, M, S, param, grad,
+                                     K, ld, lr, ptr_vec, stream);
 }
 
 #ifdef GA_DEMO_STAMPS
