@@ -448,6 +448,7 @@ def test_demo_topk_and_chunk_variants(topk, chunk, wave):
     payload = torch.zeros(1, 2 * plan.M, dtype=torch.int32, device=DEV)
     ops.demo_encode(plan, P, G, Dt, payload, 0.01, 1.0 - 1e-9, 1.0)
     gidx, gval = _payload_host(payload, plan)
+    gD = host(Dt)
     e0 = 0
     for ti, (shape, off, nel) in enumerate(zip(L.shapes, L.offsets, L.numels)):
         R, C, n1, n2 = odemo.tensor_view(shape, chunk)
@@ -461,6 +462,14 @@ def test_demo_topk_and_chunk_variants(topk, chunk, wave):
             for x in range(C // n2):
                 if margin[y, x] > 1e-5:
                     assert np.array_equal(gi[y, x], oidx[y, x]), (shape, y, x)
+        # residual delta - IDCT(top-k) (odd k: the synthesis lists' one zero entry),
+        # in the chunks whose selected set is unambiguous
+        gy, gx = R // n1, C // n2
+        Ym = np.zeros_like(Y).reshape(gy * gx, n1 * n2)
+        np.put_along_axis(Ym, oidx.reshape(gy * gx, kk), oval.reshape(gy * gx, kk), axis=1)
+        want_d = D[0, off:off + nel].reshape(shape) - odemo.decode(Ym.reshape(Y.shape), shape, chunk)
+        okel = np.repeat(np.repeat((margin > 1e-5).reshape(gy, gx), n1, axis=0), n2, axis=1).reshape(shape)
+        np.testing.assert_allclose(gD[0, off:off + nel].reshape(shape)[okel], want_d[okel], rtol=0, atol=2e-5)
         e0 += ne
 
 
