@@ -16,10 +16,13 @@ roofline = the fused ga_diloco_outer kernel: algorithmic HBM bytes per launch
 cpu_baseline = the numpy oracle's outer step (oracle/diloco.py) on rank 0, on a
         bounded slice of the same arena, single thread.
 
-Extra lines in "extras" (same timing rules, not the headline): SPARTA (K=32
-replicas per GPU, p=0.005, Philox mask), SimpleReduce (char-level nanoGPT,
-8 replicas per GPU), DeMo (GPT-2 350M, one node per GPU, chunk 64 / top-k 32),
-the inner AdamW + clip step on one GPT-2 124M arena (fused vs torch foreach).
+Extra lines in "extras" (same timing rules, not the headline): SPARTA (32
+nodes in total, 32/G per GPU, p=0.005, Philox mask: configs[3]), SimpleReduce
+(char-level nanoGPT, 8 nodes in total, 8/G per GPU: configs[1]), DeMo (GPT-2
+350M, one node per GPU, chunk 64 / top-k 32: configs[4]), the inner AdamW +
+clip step on one GPT-2 124M arena (fused vs torch foreach), and at G > 1 the
+DiLoCo step exactly as configs[2] names it -- one node per GPU, so the
+reduce-scatter/all-gather over xGMI dominates (its "xgmi" block).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-extras]
        torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -205,7 +208,10 @@ def bench_diloco(args, coll, dev):
     return out
 
 
-def bench_sparta(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
+def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m"):
+    """configs[3]: K=32 simulated nodes on one GPU, or the same 32 nodes sharded
+    32/G per GPU over G GPUs (strong: the node count is the config's)."""
+    K = max(1, K_total // coll.world)
     shapes = MODELS[model]()
     layout = ArenaLayout(shapes)
     rs = synth_replicas(layout, K, coll.rank, dev)
@@ -227,13 +233,15 @@ def bench_sparta(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
     # (rocprofv3 FETCH_SIZE/WRITE_SIZE of this kernel: 1.18 GB + 0.61 GB per step)
     sect = (64 + 32) * K * M
     return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
-            "K_local": K, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1),
+            "K_local": K, "K_total": K * coll.world, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1),
             "sector_bytes": sect, "sector_GBps": round(sect / t / 1e9, 1),
             "path": "fused select+gather+average+write-back" if coll.world == 1 else
                     f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter"}
 
 
-def bench_simple(args, coll, dev, K=8, model="gpt2-char"):
+def bench_simple(args, coll, dev, K_total=8, model="gpt2-char"):
+    """configs[1]: 8 char-level nodes, on one GPU or one per GPU (8/G per GPU)."""
+    K = max(1, K_total // coll.world)
     shapes = MODELS[model]()
     layout = ArenaLayout(shapes)
     layout.n = layout.padded_to(coll.world)
@@ -241,7 +249,7 @@ def bench_simple(args, coll, dev, K=8, model="gpt2-char"):
     eng = MeanReduce(coll, K, layout.n, dev, torch.float32)
     t = timed_loop(lambda: eng(rs.data), args.steps, args.warmup, coll)
     return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
-            "K_local": K, "model": model}
+            "K_local": K, "K_total": K * coll.world, "model": model}
 
 
 def bench_demo(args, coll, dev, model="gpt2-350m"):
@@ -356,8 +364,16 @@ def main():
     head = bench_diloco(args, coll, dev)
     extras = {}
     if not args.no_extras:
-        for name, fn in (("sparta_k32", bench_sparta), ("simple_reduce_char_k8", bench_simple),
-                         ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)):
+        runs = [("sparta_k32", bench_sparta), ("simple_reduce_char_k8", bench_simple),
+                ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
+        if coll.world > 1:  # configs[2] as named: one node per GPU, the exchange alone over xGMI
+            def diloco_1(a, c, d):
+                r = bench_diloco(argparse.Namespace(**{**vars(a), "replicas": 1}), c, d)
+                for key in ("ms_per_step", "value", "kernel_ms"):
+                    r[key] = round(r[key], 4)
+                return r
+            runs.insert(0, ("diloco_1_node_per_gpu", diloco_1))
+        for name, fn in runs:
             torch.cuda.empty_cache()
             try:
                 extras[name] = fn(args, coll, dev)
