@@ -246,6 +246,22 @@ __device__ __forceinline__ void error_feedback(T* param, const T* grad, const T*
 
 // T[s][qc] = rows of X (s = 0: rows l, 1: rows 63 - l) times F2, even (qc = 0) or
 // odd (qc = 1) frequencies d = 2 col + qc; K index of step t, half h: column 16h + t
+__device__ __forceinline__ void row_product_half(const float (&xs)[8][4], const float* Hb, int l, int h,
+                                                 f32x16 (&Ts)[2]) {
+#pragma unroll
+    for (int qc = 0; qc < 2; ++qc) {
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int q = t >> 2, e = t & 3;
+            const float u = xs[q][e], w = xs[7 - q][3 - e];
+            const float a = qc ? u - w : u + w;
+            acc = mfma(a, Hb[(16 * h + t) * kLd + 2 * l + qc], acc);
+        }
+        Ts[qc] = acc;
+    }
+}
+
 __device__ __forceinline__ void row_product(const float (&x)[2][8][4], const float* Hb, int l, int h,
                                             f32x16 (&T)[2][2]) {
 #pragma unroll
@@ -341,16 +357,16 @@ __device__ __forceinline__ uint32_t coal_off(int i, int lane, int stride) {
     return (uint32_t)(((lane >> 4) + 4 * i) * stride + 4 * (lane & 15));
 }
 
-template <typename T>
+template <typename T, int I0 = 0, int NI = 16>
 __device__ __forceinline__ void load_coal(const T* pb, int stride, bool vec, int lane, float (&o)[16][4]) {
     if (vec) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
+        for (int i = I0; i < I0 + NI; ++i)
             Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride))),
                             o[i]);
     } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
+        for (int i = I0; i < I0 + NI; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[i][e] = Elem<T>::load(at_off(pb, coal_off(i, lane, stride)) + e);
     }
@@ -402,39 +418,53 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
                 for (int e = 0; e < 4; ++e) pv[i][e] *= wd_factor;
             store_coal(param, td.cols, vec, lane, pv);
         }
-        float Dv[16][4], Gv[16][4];
-        // the chunk's loads go out ahead of the partner wave's transforms (measured
-        // -0.7% on the 350M encode; the products themselves stay at priority 0)
-        __builtin_amdgcn_s_setprio(2);
-        load_coal(delta, td.cols, vec, lane, Dv);
-        load_coal(grad, td.cols, vec, lane, Gv);
-        __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaf(lr, Gv[i][e], decay != 1.f ? Dv[i][e] * decay : Dv[i][e]);
-            tile[t4((lane >> 4) + 4 * i, lane & 15)] = make_float4(v[0], v[1], v[2], v[3]);
-        }
     }
-    WAVE_LDS_SYNC();
-    DW_PH(0);
     f32x16 Y[2][2];  // [parity of b][qc]
     {
+        // rows 0-31 (row-quads 0-7) are loaded ahead of rows 32-63, so the first
+        // half's row product runs while the second half is still in flight (the
+        // chunk's loads go out at raised priority, ahead of the partner wave's
+        // transforms; the products themselves stay at priority 0)
         const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-        float x[2][8][4];
+        float Dv[16][4], Gv[16][4];
+        __builtin_amdgcn_s_setprio(2);
+        load_coal<T, 0, 8>(delta, td.cols, vec, lane, Dv);
+        load_coal<T, 0, 8>(grad, td.cols, vec, lane, Gv);
+        __builtin_amdgcn_sched_barrier(0);  // issue order = vmcnt order: first half first
+        load_coal<T, 8, 8>(delta, td.cols, vec, lane, Dv);
+        load_coal<T, 8, 8>(grad, td.cols, vec, lane, Gv);
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int i = 0; i < 8; ++i)  // the first half is consumed only after every load is out
+            asm volatile("" : "+v"(Dv[i][0]), "+v"(Dv[i][1]), "+v"(Dv[i][2]), "+v"(Dv[i][3]), "+v"(Gv[i][0]),
+                              "+v"(Gv[i][1]), "+v"(Gv[i][2]), "+v"(Gv[i][3])::"memory");
+        __builtin_amdgcn_s_setprio(0);
+        f32x16 Tm[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int i = 8 * s; i < 8 * s + 8; ++i) {
+                if (s == 1)  // the second half's values materialise here, behind the first half's MFMAs
+                    asm volatile("" : "+v"(Dv[i][0]), "+v"(Dv[i][1]), "+v"(Dv[i][2]), "+v"(Dv[i][3]),
+                                      "+v"(Gv[i][0]), "+v"(Gv[i][1]), "+v"(Gv[i][2]), "+v"(Gv[i][3]));
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = fmaf(lr, Gv[i][e], Dv[i][e] * decay);  // * 1.0f is exact
+                tile[t4((lane >> 4) + 4 * i, lane & 15)] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+            WAVE_LDS_SYNC();
+            float xs[8][4];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const float4 v = tile[t4(s ? 63 - l : l, blk(h, q))];
-                x[s][q][0] = v.x;
-                x[s][q][1] = v.y;
-                x[s][q][2] = v.z;
-                x[s][q][3] = v.w;
+                xs[q][0] = v.x;
+                xs[q][1] = v.y;
+                xs[q][2] = v.z;
+                xs[q][3] = v.w;
             }
-        f32x16 Tm[2][2];
-        row_product(x, Hb, l, h, Tm);
+            row_product_half(xs, Hb, l, h, Tm[s]);
+            // keep the first half's MFMAs ahead of the second half's loads' uses
+            if (s == 0) __builtin_amdgcn_sched_barrier(0);
+        }
         DW_PH(1);
 #pragma unroll
         for (int qc = 0; qc < 2; ++qc) {

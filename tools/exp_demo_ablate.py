@@ -5,7 +5,10 @@ N(0, 1e-4) one, or (--evolve N) the delta after N encodes of one fixed grad
 (the bench's regime: the removed top-k flattens the spectrum step by step).
 With the stamps build (build/libgym_amd_stamps.so) also counts the chunks that
 took the all-keys selection (more than 128 candidates).
-Usage: python tools/exp_demo_ablate.py [--evolve N] build/abl/lib_*.so"""
+--codec N instead runs N whole DeMo steps first (encode + decode, the decode
+writing sign(g) into the grad buffer, as bench.py's DeMo line does) and times
+the encode from that state.
+Usage: python tools/exp_demo_ablate.py [--evolve N | --codec N] build/abl/lib_*.so"""
 import ctypes
 import os
 import sys
@@ -31,9 +34,11 @@ def bind(path):
 
 def main():
     args = sys.argv[1:]
-    evolve = 0
+    evolve = codec_steps = 0
     if args and args[0] == "--evolve":
         evolve, args = int(args[1]), args[2:]
+    if args and args[0] == "--codec":
+        codec_steps, args = int(args[1]), args[2:]
     libs = args
     dev = torch.device("cuda:0")
     layout = ArenaLayout(MODELS["gpt2-350m"]())
@@ -60,6 +65,18 @@ def main():
         fns[path] = enc
     for _ in range(evolve):
         fns[libs[0]]()
+    if codec_steps:  # bench.py's regime: P, G as bench_demo builds them, the decode writes sign into G
+        from gym_amd.comm import Collective
+        from gym_amd.engine import DeMoCodec
+        sys.argv = sys.argv[:1]
+        import bench
+        P.copy_(bench.synth_replicas(layout, 1, 0, dev).data[0, :layout.n])
+        G.copy_(bench.synth_replicas(layout, 1, 7, dev).data[0, :layout.n])
+        D.zero_()
+        codec = DeMoCodec(Collective(), 1, layout, dev)
+        for _ in range(codec_steps):
+            codec(P.view(1, -1), G.view(1, -1), D.view(1, -1), 1e-3, 0.999, 0.0)
+        evolve = f"codec {codec_steps}"
     D0 = D.clone()
     st = os.path.join(ROOT, "build", "libgym_amd_stamps.so")
     if os.path.exists(st):
