@@ -8,7 +8,9 @@ took the all-keys selection (more than 128 candidates).
 --codec N instead runs N whole DeMo steps first (encode + decode, the decode
 writing sign(g) into the grad buffer, as bench.py's DeMo line does) and times
 the encode from that state.
-Usage: python tools/exp_demo_ablate.py [--evolve N | --codec N] build/abl/lib_*.so"""
+--decode S times ga_demo_decode_sym instead, over S distinct gathered payloads
+(S nodes' encodes of independent deltas), parameters restored before each run.
+Usage: python tools/exp_demo_ablate.py [--evolve N | --codec N | --decode S] build/abl/lib_*.so"""
 import ctypes
 import os
 import sys
@@ -39,6 +41,9 @@ def main():
         evolve, args = int(args[1]), args[2:]
     if args and args[0] == "--codec":
         codec_steps, args = int(args[1]), args[2:]
+    dec_S = 0
+    if args and args[0] == "--decode":
+        dec_S, args = int(args[1]), args[2:]
     libs = args
     dev = torch.device("cuda:0")
     layout = ArenaLayout(MODELS["gpt2-350m"]())
@@ -51,6 +56,13 @@ def main():
     pl = torch.zeros(2 * plan.M, dtype=torch.int32, device=dev)
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     vp = ctypes.c_void_p
+    gathered = None
+    if dec_S:  # S nodes' payloads from independent deltas (the default library's encode)
+        from gym_amd import ops
+        gathered = torch.zeros(dec_S, 2 * plan.M, dtype=torch.int32, device=dev)
+        for j in range(dec_S):
+            Dj = torch.randn(layout.n, device=dev) * 1e-4
+            ops.demo_encode(plan, P.view(1, -1), G.view(1, -1), Dj.view(1, -1), gathered[j:j + 1], 1e-3, 0.999, 1.0)
     fns = {}
     for path in libs:
         L = bind(path)
@@ -62,7 +74,14 @@ def main():
                                       1e-3, 0.999, 1.0, vp(pl.data_ptr()), 2 * plan.M, plan.M, s)
             assert rc == 0
 
-        fns[path] = enc
+        def dec(L=L):
+            rc = L.ga_demo_decode_sym(0, vp(plan.desc64.data_ptr()), plan.n64tensors, plan.n64chunks,
+                                      vp(plan.groups.data_ptr()), plan.ngroups, vp(plan.F64.data_ptr()),
+                                      vp(gathered.data_ptr()), gathered.stride(0), plan.M, dec_S,
+                                      vp(P.data_ptr()), vp(G.data_ptr()), 1, layout.n, 1e-3, s)
+            assert rc == 0
+
+        fns[path] = dec if dec_S else enc
     for _ in range(evolve):
         fns[libs[0]]()
     if codec_steps:  # bench.py's regime: P, G as bench_demo builds them, the decode writes sign into G
@@ -78,8 +97,9 @@ def main():
             codec(P.view(1, -1), G.view(1, -1), D.view(1, -1), 1e-3, 0.999, 0.0)
         evolve = f"codec {codec_steps}"
     D0 = D.clone()
+    P0 = P.clone()
     st = os.path.join(ROOT, "build", "libgym_amd_stamps.so")
-    if os.path.exists(st):
+    if os.path.exists(st) and not dec_S:
         S = bind(st)
         S.ga_demo_stamps_set_wave.argtypes = [ctypes.c_void_p]
         stamps = torch.zeros(plan.nchunks * 16, dtype=torch.int64, device=dev)
@@ -101,7 +121,7 @@ def main():
     torch.cuda.synchronize()
     for _ in range(25):  # interleaved rounds: box clock drift hits every build alike
         for p, f in fns.items():
-            D.copy_(D0)
+            (P if dec_S else D).copy_(P0 if dec_S else D0)
             e0.record()
             f()
             e1.record()
@@ -109,7 +129,7 @@ def main():
             times[p].append(e0.elapsed_time(e1))
     for p in libs:
         t = sorted(times[p])
-        print(f"{os.path.basename(p):28s} encode median {t[len(t) // 2]:.4f} ms  min {t[0]:.4f}", flush=True)
+        print(f"{os.path.basename(p):28s} {'decode S=%d' % dec_S if dec_S else 'encode'} median {t[len(t) // 2]:.4f} ms  min {t[0]:.4f}", flush=True)
 
 
 if __name__ == "__main__":
