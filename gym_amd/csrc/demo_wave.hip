@@ -326,10 +326,15 @@ __device__ __forceinline__ void synth_batch(const uint2* lst, int q, int cH, int
 // (whole pairs only: no MFMA spent on padding beyond one zero entry)
 __device__ __forceinline__ void synth_list(const uint2* lst, int np, int cH, int l, int h, const float* Hb,
                                            f32x16& acc) {
+    static_assert(kSynB == 2 || kSynB == 4 || kSynB == 8, "synthesis tail handles 4/2/1 pairs");
     int q = 0;
     for (; q + kSynB <= np; q += kSynB) synth_batch<kSynB>(lst, q, cH, l, h, Hb, acc);
-    const int rem = np - q;
-    if (rem >= 2) {
+    const int rem = np - q;  // < kSynB
+    if (kSynB > 4 && (rem & 4)) {
+        synth_batch<4>(lst, q, cH, l, h, Hb, acc);
+        q += 4;
+    }
+    if (kSynB > 2 && (rem & 2)) {
         synth_batch<2>(lst, q, cH, l, h, Hb, acc);
         q += 2;
     }
