@@ -385,7 +385,7 @@ def main():
             dist.destroy_process_group()
         return
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and coll.world == 1:  # the CPU leg is timed at N=1 only
         cpu = cpu_baseline_diloco(head["n_params"], args.replicas)
     K_total = head["K_total"]
     line = {

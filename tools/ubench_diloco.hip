@@ -144,6 +144,35 @@ __global__ __launch_bounds__(256) void v_chunk(const float* src, long ld, long n
     }
 }
 
+// v_chunk with an XCD-aware block order: blocks b and b+8 share an XCD (round-robin
+// dispatch), so block b takes chunk (b % 8) * per + b / 8 and each XCD streams one
+// contiguous eighth of the arena (fewer pages per XCD's TLB, longer DRAM runs)
+template <int K, int CH>
+__global__ __launch_bounds__(256) void v_chunk_xcd(const float* src, long ld, long n, float* master, float* mom, OP op,
+                                                   float* dst) {
+    const long nv = n >> 2;
+    const long per = gridDim.x >> 3;
+    const long cb = (long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    const long lo = cb * CH;
+    const long hi = lo + CH < nv ? lo + CH : nv;
+    for (long v = lo + threadIdx.x; v < hi; v += 256) {
+        float4 x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[k] = reinterpret_cast<const float4*>(src + k * ld)[v];
+        float4 m = reinterpret_cast<const float4*>(master)[v], b = reinterpret_cast<const float4*>(mom)[v];
+        float a[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < K; ++k) { a[0] += x[k].x; a[1] += x[k].y; a[2] += x[k].z; a[3] += x[k].w; }
+        float4 o;
+        o.x = upd(a[0], m.x, b.x, op); o.y = upd(a[1], m.y, b.y, op);
+        o.z = upd(a[2], m.z, b.z, op); o.w = upd(a[3], m.w, b.w, op);
+        reinterpret_cast<float4*>(master)[v] = m;
+        reinterpret_cast<float4*>(mom)[v] = b;
+#pragma unroll
+        for (int k = 0; k < K; ++k) reinterpret_cast<float4*>(dst + k * ld)[v] = o;
+    }
+}
+
 // persistent contiguous ranges: workgroup b streams vectors [b*per, (b+1)*per)
 template <int K, bool NTL>
 __global__ __launch_bounds__(256) void v_persist(const float* src, long ld, long n, float* master, float* mom, OP op,
@@ -232,6 +261,21 @@ int main() {
     {                                                                                                     \
         float ms = time_ms([&] { v_persist<K, NTL><<<G, 256>>>(src, ld, n, master, mom, op, src); }, reps);  \
         printf("persist G=%d ntl=%d: %.3f ms  %.0f GB/s\n", G, NTL, ms, bytes / ms / 1e6);                 \
+    }
+#define RUNX(CH)                                                                                          \
+    {                                                                                                     \
+        int g = (int)(((n / 4 + CH - 1) / CH + 7) / 8 * 8);                                               \
+        float ms = time_ms([&] { v_chunk_xcd<K, CH><<<g, 256>>>(src, ld, n, master, mom, op, src); }, reps); \
+        printf("chunk-xcd CH=%d grid %6d: %.3f ms  %.0f GB/s\n", CH, g, ms, bytes / ms / 1e6);           \
+    }
+    if (getenv("XCD_AB")) {
+        for (int rep = 0; rep < 3; ++rep) {
+            RUNC(1024, 1, false)
+            RUNX(1024)
+            RUNX(2048)
+            RUNX(512)
+        }
+        return 0;
     }
     RUNP(512, false)
     RUNP(1024, false)
