@@ -950,12 +950,73 @@ __device__ __forceinline__ float sgnf(float g) { return (float)((g > 0.f) - (g <
 // the signs (layout C, read from the tile where used) -> p -= lr * sign, grad = sign,
 // for each of K replicas; a full 64-row chunk's replica 0 comes in pre (loaded before
 // the chunk's transform, so the load latency hides behind it)
+// a chunk's parameters held as loaded (4 elements per Vec4<T>: 64 VGPRs for fp32, 32 for
+// bf16), widened to fp32 only where the update consumes them
+template <typename T>
+using PRaw = typename Vec4<T>::type[16];
+
+template <typename T>
+__device__ __forceinline__ void load_coal_raw(const T* pb, int stride, bool vec, int lane, PRaw<T>& o) {
+    if (vec) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            o[i] = *reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride)));
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            float f[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f[e] = Elem<T>::load(at_off(pb, coal_off(i, lane, stride)) + e);
+            o[i] = Vec4<T>::pack(f);  // exact: f holds T values
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_quad(T* pb, int i, int stride, bool vec, int lane, const float (&f)[4]) {
+    T* a = at_off(pb, coal_off(i, lane, stride));
+    if (vec) {
+        *reinterpret_cast<typename Vec4<T>::type*>(a) = Vec4<T>::pack(f);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Elem<T>::store(a + e, f[e]);
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, int stride, bool vec, float lr,
-                                            int lane, float (&p)[16][4]) {
+                                            int lane, const PRaw<T>& raw) {
+    if constexpr (sizeof(typename Vec4<T>::type) < 16) {
+        // packed (bf16) rows: widen, update and store one row quad at a time, so the
+        // fp32 copy of the chunk is never live whole (244 -> 116 B/lane of spill at 8 sources)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+            float f[4];
+            Vec4<T>::unpack(raw[i], f);
+            f[0] = fmaf(-lr, v.x, f[0]);
+            f[1] = fmaf(-lr, v.y, f[1]);
+            f[2] = fmaf(-lr, v.z, f[2]);
+            f[3] = fmaf(-lr, v.w, f[3]);
+            store_quad(pr, i, stride, vec, lane, f);
+        }
+        if (gr) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+                const float f[4] = {v.x, v.y, v.z, v.w};
+                store_quad(gr, i, stride, vec, lane, f);
+            }
+        }
+        return;
+    }
+    // fp32: every fused update first, then the 16 stores back to back (measured: the
+    // per-quad form above costs fp32 ~20% here)
+    float p[16][4];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+        Vec4<T>::unpack(raw[i], p[i]);
         p[i][0] = fmaf(-lr, v.x, p[i][0]);
         p[i][1] = fmaf(-lr, v.y, p[i][1]);
         p[i][2] = fmaf(-lr, v.z, p[i][2]);
@@ -977,12 +1038,12 @@ __device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, in
 
 template <typename T>
 __device__ __forceinline__ void apply_signs(const float4* tile, T* param, T* grad, int64_t K, int64_t ld, int stride,
-                                            bool vec, int nrows, float lr, int lane, float (&pre)[16][4]) {
+                                            bool vec, int nrows, float lr, int lane, const PRaw<T>& pre) {
     if (nrows == 64) {
         sign_update(tile, param, grad, stride, vec, lr, lane, pre);
         for (int64_t r = 1; r < K; ++r) {
-            float p[16][4];
-            load_coal(param + r * ld, stride, vec, lane, p);
+            PRaw<T> p;
+            load_coal_raw(param + r * ld, stride, vec, lane, p);
             sign_update(tile, param + r * ld, grad ? grad + r * ld : nullptr, stride, vec, lr, lane, p);
         }
         return;
@@ -1071,8 +1132,8 @@ __device__ __forceinline__ void dchunk_entries(const ga_demo_tensor& td, int c, 
 
 template <typename T>
 __device__ __forceinline__ void dchunk_params(const ga_demo_tensor& td, int c, const T* param, int ptr_vec,
-                                              float (&p0)[16][4]) {
-    load_coal(param + chunk_base(td, c), td.cols, chunk_vec(td, ptr_vec), lane_id(), p0);
+                                              PRaw<T>& p0) {
+    load_coal_raw(param + chunk_base(td, c), td.cols, chunk_vec(td, ptr_vec), lane_id(), p0);
 }
 
 // sign(g) of chunk c into the tile (swizzled row-major) from the entries in `in`
@@ -1188,8 +1249,8 @@ __device__ __forceinline__ void dgroup(const ga_demo_rowgroup& rg, const int32_t
     const bool vec = ptr_vec && (rg.offset % 4 == 0);
     float4* tile = reinterpret_cast<float4*>(W.tile);
     const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-    float pre[16][4];  // a full group's replica 0, in flight behind the transform
-    if (rows == 64) load_coal(param + rg.offset, 64, vec, lane, pre);
+    PRaw<T> pre;  // a full group's replica 0, in flight behind the transform
+    if (rows == 64) load_coal_raw(param + rg.offset, 64, vec, lane, pre);
 #pragma unroll
     for (int i = 0; i < 16; ++i) tile[i * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     reinterpret_cast<uint4*>(W.aux)[lane] = make_uint4(0u, 0u, 0u, 0u);
@@ -1256,7 +1317,7 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     // them) and its parameters right after them, a whole transform ahead of their use
     if (job < nchunks) {
         DecIn<MS> cur;
-        float p0[16][4];
+        PRaw<T> p0;
         tix = find_tensor(tens, ntens, tix, (int)job);
         ga_demo_tensor td = tens[tix];
         dchunk_entries(td, (int)job - td.chunk_start, payload, pstride, M, S, cur);
