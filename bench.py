@@ -363,7 +363,7 @@ def main():
 
     head = bench_diloco(args, coll, dev)
     extras = {}
-    if not args.no_extras:
+    if not args.no_extras and args.only != "diloco":
         runs = [("sparta_k32", bench_sparta), ("simple_reduce_char_k8", bench_simple),
                 ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
         if coll.world > 1:  # configs[2] as named: one node per GPU, the exchange alone over xGMI
