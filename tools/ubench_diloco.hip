@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -219,7 +220,69 @@ float time_ms(F f, int reps) {
     return ms / reps;
 }
 
+// ALLOC=one|split|pad1g|contig: the [K, ld] replica set as one buffer, as K separate
+// buffers (row pointers passed in a table), or one buffer with rows 1 GiB apart
+template <int K>
+__global__ __launch_bounds__(256) void v_rows(const float* const* rows, long n, float* master, float* mom, OP op) {
+    const long nv = n >> 2;
+    const long lo = (long)blockIdx.x * 1024;
+    const long hi = lo + 1024 < nv ? lo + 1024 : nv;
+    for (long v = lo + threadIdx.x; v < hi; v += 256) {
+        float4 x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[k] = reinterpret_cast<const float4*>(rows[k])[v];
+        float4 m = reinterpret_cast<const float4*>(master)[v], b = reinterpret_cast<const float4*>(mom)[v];
+        float a[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < K; ++k) { a[0] += x[k].x; a[1] += x[k].y; a[2] += x[k].z; a[3] += x[k].w; }
+        float4 o;
+        o.x = upd(a[0], m.x, b.x, op); o.y = upd(a[1], m.y, b.y, op);
+        o.z = upd(a[2], m.z, b.z, op); o.w = upd(a[3], m.w, b.w, op);
+        reinterpret_cast<float4*>(master)[v] = m;
+        reinterpret_cast<float4*>(mom)[v] = b;
+#pragma unroll
+        for (int k = 0; k < K; ++k) reinterpret_cast<float4*>(const_cast<float*>(rows[k]))[v] = o;
+    }
+}
+
+static int alloc_mode() {
+    const char* mode = getenv("ALLOC");
+    if (!mode) return -1;
+    const int K = 8;
+    const long n = 124475904;
+    std::vector<float*> rows(K);
+    float *master, *mom;
+    CK(hipMalloc(&master, sizeof(float) * n));
+    CK(hipMalloc(&mom, sizeof(float) * n));
+    CK(hipMemset(master, 0, sizeof(float) * n));
+    CK(hipMemset(mom, 0, sizeof(float) * n));
+    const std::string m(mode);
+    if (m == "contig") {  // one buffer, physically contiguous pages requested from the driver
+        float* base;
+        CK(hipExtMallocWithFlags((void**)&base, sizeof(float) * (K * n), hipDeviceMallocContiguous));
+        for (int k = 0; k < K; ++k) rows[k] = base + k * n;
+    } else if (m == "split") {
+        for (int k = 0; k < K; ++k) CK(hipMalloc(&rows[k], sizeof(float) * n));
+    } else {
+        const long ld = m == "pad1g" ? (1L << 28) : n;  // 2^28 floats = 1 GiB
+        float* base;
+        CK(hipMalloc(&base, sizeof(float) * (K * ld)));
+        for (int k = 0; k < K; ++k) rows[k] = base + k * ld;
+    }
+    for (int k = 0; k < K; ++k) CK(hipMemset(rows[k], 0, sizeof(float) * n));
+    float** drows;
+    CK(hipMalloc(&drows, sizeof(float*) * K));
+    CK(hipMemcpy(drows, rows.data(), sizeof(float*) * K, hipMemcpyHostToDevice));
+    OP op{8.f, 0.7f, 0.9f};
+    const double bytes = (2.0 * K + 4.0) * 4.0 * n;
+    const int g = (int)((n / 4 + 1023) / 1024);
+    float ms = time_ms([&] { v_rows<K><<<g, 256>>>(drows, n, master, mom, op); }, 20);
+    printf("alloc=%s %.3f ms %.0f GB/s\n", mode, ms, bytes / ms / 1e6);
+    return 0;
+}
+
 int main() {
+    if (alloc_mode() == 0) return 0;
     const int K = 8;
     const long n = 124475904;  // GPT-2 124M arena
     const long ld = n;
