@@ -37,7 +37,29 @@ struct Pred {
     const uint8_t* mask;  // null -> Philox
     uint2 key;
     uint32_t it_lo, it_hi, thr;
+    const int64_t* skip;  // Philox: sorted disjoint [lo, hi) element ranges never selected
+    int32_t nskip;
 };
+
+// Clear the bits of the 16 elements at e0 that fall in a skipped range
+// (tensors without a gradient, sparta.py:29-30).  Binary search for the first
+// range ending after e0; a 16-element group meets at most a few ranges.
+__device__ __forceinline__ uint32_t clear_skipped(const Pred& P, int64_t e0, uint32_t bits) {
+    int lo = 0, hi = P.nskip;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (P.skip[2 * mid + 1] <= e0) lo = mid + 1;
+        else hi = mid;
+    }
+    for (int r = lo; r < P.nskip && bits; ++r) {
+        const int64_t a = P.skip[2 * r], b = P.skip[2 * r + 1];
+        if (a >= e0 + 16) break;
+        const int s = a > e0 ? (int)(a - e0) : 0;
+        const int t = b < e0 + 16 ? (int)(b - e0) : 16;
+        bits &= ~(((1u << t) - 1u) & ~((1u << s) - 1u));
+    }
+    return bits;
+}
 
 // Selection bits of the 16 elements starting at element `e0` (e0 % 16 == 0).
 __device__ __forceinline__ uint32_t pred_bits16(const Pred& P, int64_t e0, int64_t n) {
@@ -65,6 +87,7 @@ __device__ __forceinline__ uint32_t pred_bits16(const Pred& P, int64_t e0, int64
             bits |= ((r.w >> 8) < P.thr) << (4 * q + 3);
         }
         if (e0 + 16 > n) bits &= (n - e0) >= 16 ? 0xffffu : ((1u << (uint32_t)(n - e0)) - 1u);
+        if (P.nskip) bits = clear_skipped(P, e0, bits);
     }
     return bits;
 }
@@ -308,7 +331,8 @@ extern "C" GA_API uint32_t ga_sparta_threshold(double p) {
 
 extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld, int64_t n,
                                        const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                       uint32_t threshold, int64_t cap, int32_t* idx, void* vals,
+                                       uint32_t threshold, const int64_t* skip, int64_t nskip,
+                                       int64_t cap, int32_t* idx, void* vals,
                                        int64_t* count, void* work, hipStream_t stream) {
     clear_error();
     GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "ga_sparta_select: n=%lld out of int32 index range", (long long)n);
@@ -317,6 +341,7 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     GA_REQUIRE(K == 1 || ld >= n, "ga_sparta_select: ld < n");
     GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_select: threshold > 2^24");
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_select: mask must be 16-byte aligned");
+    GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_select: bad skip table");
     if (n == 0) return hipMemsetAsync(count, 0, 2 * sizeof(int64_t), stream) == hipSuccess ? GA_OK : GA_EHIP;
     GA_REQUIRE(src && idx && vals, "ga_sparta_select: null src/idx/vals");
     Pred P;
@@ -325,6 +350,8 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     P.it_lo = (uint32_t)iteration;
     P.it_hi = (uint32_t)(iteration >> 32);
     P.thr = threshold;
+    P.skip = skip;
+    P.nskip = (int32_t)nskip;
     switch (dtype) {
         case GA_F32: return launch_select<float>(src, K, ld, n, P, cap, idx, vals, count, work, 0.f, stream);
         case GA_BF16:
@@ -335,7 +362,8 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
 
 extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
                                               const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                              uint32_t threshold, float divisor, int32_t* idx, void* vals,
+                                              uint32_t threshold, const int64_t* skip, int64_t nskip,
+                                              float divisor, int32_t* idx, void* vals,
                                               int64_t cap, int64_t* count, void* work, hipStream_t stream) {
     clear_error();
     GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "ga_sparta_average_local: n=%lld out of range", (long long)n);
@@ -344,6 +372,7 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
     GA_REQUIRE(K == 1 || ld >= n, "ga_sparta_average_local: ld < n");
     GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_average_local: threshold > 2^24");
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_average_local: mask alignment");
+    GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_average_local: bad skip table");
     GA_REQUIRE((idx == nullptr && vals == nullptr && count == nullptr) || (idx && vals && count && work),
                "ga_sparta_average_local: idx, vals, count and work go together");
     if (n == 0) return GA_OK;
@@ -354,6 +383,8 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
     P.it_lo = (uint32_t)iteration;
     P.it_hi = (uint32_t)(iteration >> 32);
     P.thr = threshold;
+    P.skip = skip;
+    P.nskip = (int32_t)nskip;
     switch (dtype) {
         case GA_F32: return launch_select<float>(reps, K, ld, n, P, cap, idx, vals, count, work, divisor, stream);
         case GA_BF16:

@@ -9,7 +9,7 @@ node count is K_total = world * K_local.
 
   MeanReduce   SimpleReduce grads, FedAvg params     strategy.py:128-142, federated_averaging.py:53-69
   DiLoCoOuter  fused outer SGD/Nesterov step        diloco.py:34-76
-  Sparta       sparse average (Philox or mask)      sparta.py:113-131
+  Sparta       sparse average (Philox or mask)      sparta.py:24-44
   DeMoCodec    DCT encode/top-k + gather + decode   demo_impl/demo.py:142-209
 """
 import math
@@ -245,13 +245,19 @@ class Sparta:
             self.vals = torch.empty(cap, dtype=self.dtype, device=self.device)
 
     def check(self):
-        """Raise if an earlier Philox step selected more than the capacity."""
+        """Raise if an earlier Philox step selected more than the capacity.
+
+        The capacity is mean + 16 sigma + 1024 of the Binomial(n, p) count, so
+        an overflow has probability < 1e-50 per step; the flag is still read
+        back (asynchronously, no host sync in the step) and raised at the
+        start of the next step, or by an explicit check() -- the strategies
+        call it when training ends, so even the last step is covered."""
         if self._flag_event is not None:
             self._flag_event.synchronize()
             if int(self._flag_host[1]) != 0:
                 raise RuntimeError(f"SPARTA: {int(self._flag_host[0])} elements selected > capacity {self.cap}")
 
-    def __call__(self, reps, seed=0, iteration=0, mask=None):
+    def __call__(self, reps, seed=0, iteration=0, mask=None, skip=None):
         n = self.n
         if mask is not None:  # reference mask (rank 0's); exact count known from the mask
             cap = max(1, int(mask[:n].sum().item()))
@@ -262,10 +268,10 @@ class Sparta:
             cap_used = self.cap
         if self.coll.world == 1:  # every node is a local replica: one fused pass, no exchange
             ops.sparta_average_local(reps, n, float(self.K_total), mask=mask, seed=seed, iteration=iteration,
-                                     p=self.p)
+                                     p=self.p, skip=skip)
             return
         ops.sparta_select(reps, n, cap_used, self.idx, self.vals, self.count, self.work, mask=mask, seed=seed,
-                          iteration=iteration, p=self.p)
+                          iteration=iteration, p=self.p, skip=skip)
         self.coll.all_reduce_(self.vals[:cap_used])
         ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps)
         if mask is None:  # overflow flag read back asynchronously, checked next step

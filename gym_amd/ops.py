@@ -104,12 +104,23 @@ def sparta_workspace(n, device):
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
-def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0):
-    """Compact the selected elements of [0, n) (mask != 0, or the Philox draw)
-    into idx (int32) and vals (= sum over the replicas of src); count[0] = number
-    selected, count[1] = overflow flag."""
+def _skip_table(skip):
+    """skip: None or an int64 device tensor [R, 2] of sorted disjoint [lo, hi)
+    element ranges the Philox draw never selects."""
+    if skip is None or skip.numel() == 0:
+        return None, 0
+    if skip.dtype != torch.int64 or skip.dim() != 2 or skip.shape[1] != 2 or not skip.is_contiguous():
+        raise ValueError("sparta skip table must be a contiguous int64 [R, 2] tensor")
+    return skip, skip.shape[0]
+
+
+def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0, skip=None):
+    """Compact the selected elements of [0, n) (mask != 0, or the Philox draw
+    outside the `skip` ranges) into idx (int32) and vals (= sum over the
+    replicas of src); count[0] = number selected, count[1] = overflow flag."""
     src2 = _as2d(src)
-    _gpu(src2, idx, vals, count, work, mask)
+    _gpu(src2, idx, vals, count, work, mask, skip)
+    skip, nskip = _skip_table(skip)
     K, ld = _rows_ld(src2)
     if idx.dtype != torch.int32 or count.dtype != torch.int64 or count.numel() < 2:
         raise TypeError("sparta_select: idx int32, count int64[2]")
@@ -122,17 +133,19 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
             raise ValueError("sparta_select: mask must be uint8/bool with >= n elements")
     thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
     check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, int(n), _p(mask), int(seed) & (2**64 - 1),
-                                 int(iteration) & (2**64 - 1), thr, int(cap), _p(idx), _p(vals), _p(count),
+                                 int(iteration) & (2**64 - 1), thr, _p(skip), nskip, int(cap), _p(idx), _p(vals),
+                                 _p(count),
                                  _p(work), _stream()), "ga_sparta_select")
 
 
 def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0, idx=None, vals=None, cap=0,
-                         count=None, work=None):
+                         count=None, work=None, skip=None):
     """Single-process SPARTA step over [K, ld] replicas: selected elements of
     every replica <- (sum over replicas) / divisor, one pass (optional packed
     idx/vals/count outputs as sparta_select)."""
     r2 = _as2d(reps)
-    _gpu(r2, mask, idx, vals, count, work)
+    _gpu(r2, mask, idx, vals, count, work, skip)
+    skip, nskip = _skip_table(skip)
     K, ld = _rows_ld(r2)
     if mask is not None and (mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n):
         raise ValueError("sparta_average_local: mask must be uint8/bool with >= n elements")
@@ -143,7 +156,8 @@ def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0
             raise ValueError("sparta_average_local: output buffers too small")
     thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
     check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, int(n), _p(mask), int(seed) & (2**64 - 1),
-                                        int(iteration) & (2**64 - 1), thr, float(divisor), _p(idx), _p(vals),
+                                        int(iteration) & (2**64 - 1), thr, _p(skip), nskip, float(divisor),
+                                        _p(idx), _p(vals),
                                         int(cap), _p(count), _p(work), _stream()), "ga_sparta_average_local")
 
 

@@ -13,9 +13,10 @@ its own data shard (DistributedSampler(num_replicas=num_nodes, rank=node) or
 the dataset factory called with the node's rank), gradient accumulation over
 batch_size // minibatch_size minibatches with `grad /= batch_size /
 minibatch_size`, its own clip_grad_norm_, then the strategy step.  Supported
-strategies: SimpleReduce, DiLoCo (SGD-family outer optimizer), SPARTA (Philox
-mask stream), FedAvg without islands, DeMo.  Anything else runs on the
-process-per-node path (ReplicaRunner.supports).
+strategies: SimpleReduce, DiLoCo (SGD-family outer optimizer), SPARTA (every
+selector: the torch-drawn masks of node 0 -- the reference uses rank 0's --
+or the Philox stream), FedAvg without islands, DeMo.  Anything else runs on
+the process-per-node path (ReplicaRunner.supports).
 """
 import copy
 
@@ -70,8 +71,7 @@ class ReplicaRunner:
     @staticmethod
     def supports(strategy):
         if isinstance(strategy, SPARTAStrategy):
-            sel = strategy.index_selector
-            return isinstance(sel, RandomIndexSelector) and sel.mask_source == "philox"
+            return True
         if isinstance(strategy, FedAvgStrategy):
             return strategy.island_size is None
         if isinstance(strategy, DiLoCoStrategy):
@@ -124,9 +124,14 @@ class ReplicaRunner:
                 self.mean = MeanReduce(self.coll, self.K, ld, dev, dt)
             elif isinstance(s, SPARTAStrategy):
                 self.sparta = Sparta(self.coll, self.K, ld, dev, dt, s.index_selector.p)
-                t = torch.tensor([torch.initial_seed() & (2**63 - 1)], dtype=torch.int64, device=dev)
-                self.coll.broadcast_(t, 0)
-                self.seed = int(t.item())
+                sel = s.index_selector
+                self.philox = isinstance(sel, RandomIndexSelector) and sel.mask_source == "philox"
+                if self.philox:
+                    t = torch.tensor([torch.initial_seed() & (2**63 - 1)], dtype=torch.int64, device=dev)
+                    self.coll.broadcast_(t, 0)
+                    self.seed = int(t.item())
+                else:
+                    self.mask = torch.zeros(ld, dtype=torch.uint8, device=dev)
                 self.iteration = 0
         # the strategy's LR schedule on every optimizer (strategy.py:75-112)
         for o in (self.optim.opts if isinstance(self.optim, _PerNodeOptim) else [self.optim]):
@@ -158,7 +163,10 @@ class ReplicaRunner:
                 self.outer(P)
         elif isinstance(s, SPARTAStrategy):
             self._inner()
-            self.sparta(P, seed=self.seed, iteration=self.iteration)
+            if self.philox:
+                self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
+            else:
+                self.sparta(P, mask=self._build_mask())
             self.iteration += 1
         elif isinstance(s, FedAvgStrategy):
             self._inner()
@@ -170,6 +178,35 @@ class ReplicaRunner:
             for cb in s.lr_callbacks:
                 cb(self.lr_scheds[0].get_last_lr()[0])
         s.local_step += 1
+
+    def _grad_less(self):
+        """Indices of node 0's tensors without a gradient (skipped, sparta.py:29-30)."""
+        a0 = self.ra.arenas[0]
+        return [i for i, p in enumerate(a0.params) if not p.requires_grad or p.grad is None]
+
+    def _skip_table(self):
+        L = self.ra.layout
+        rng = []
+        for i in self._grad_less():
+            lo, hi = L.offsets[i], L.offsets[i] + L.numels[i]
+            if rng and rng[-1][1] == lo:
+                rng[-1][1] = hi
+            else:
+                rng.append([lo, hi])
+        return torch.tensor(rng, dtype=torch.int64, device=self.ra.device).view(-1, 2) if rng else None
+
+    def _build_mask(self):
+        """Node 0's selector masks (the reference broadcasts rank 0's,
+        sparta.py:32-37) as one uint8 arena, broadcast to the other processes."""
+        a0 = self.ra.arenas[0]
+        skip = set(self._grad_less())
+        for i, (p, v) in enumerate(zip(a0.params, self.ra.layout.views(self.mask))):
+            if i in skip:
+                v.zero_()
+            else:
+                v.copy_(self.s.index_selector.get_indices(p, self.iteration))
+        self.coll.broadcast_(self.mask, 0)
+        return self.mask
 
     def _inner(self):
         if isinstance(self.optim, ArenaAdam):
@@ -307,6 +344,8 @@ class ReplicaTrainNode:
                 self.logger.increment_step()
             if world > 1:
                 dist.barrier()
+        if hasattr(self.runner, "sparta"):
+            self.runner.sparta.check()
         self._evaluate()
         return [m.state_dict() for m in self.models]
 

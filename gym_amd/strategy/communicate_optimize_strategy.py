@@ -50,6 +50,12 @@ class CommunicateOptimizeStrategy(Strategy):
         for m in self.communication_modules:
             m.communicate(self.model, self.rank, self.num_nodes, self.local_step)
 
+    def finish(self):
+        for m in self.communication_modules:
+            fin = getattr(m, "finish", None)
+            if fin is not None:
+                fin()
+
     def _init_node(self, model, rank, num_nodes):
         super()._init_node(model, rank, num_nodes)
         self._bind_arena(model)

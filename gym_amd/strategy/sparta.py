@@ -1,26 +1,34 @@
 """SPARTA: after every inner step, average a random sparse subset of the
 parameters across nodes.
 
-API of exogym/strategy/sparta.py:14-282: SparseCommunicator(index_selector),
-SPARTAStrategy(inner_optim=None, p_sparta=0.005, **kwargs), IndexSelector,
-RandomIndexSelector, ShuffledSequentialIndexSelector, PartitionedIndexSelector.
+API of exogym/strategy/sparta.py:14-193: SparseCommunicator(index_selector)
+(:14-47), SPARTAStrategy(inner_optim=None, p_sparta=0.005, **kwargs) (:50-66),
+IndexSelector (:69-77), RandomIndexSelector (:80-85),
+ShuffledSequentialIndexSelector (:88-136), PartitionedIndexSelector (:139-193).
 
-The reference loops over every tensor: draw a Bernoulli(p) mask, broadcast the
-bool mask from rank 0, gather, all-reduce, divide, masked_scatter.  Here one
-select+gather kernel runs over the whole arena, ONE all-reduce moves the
-packed values (about p*N elements), one scatter kernel writes them back.
+The reference loops over every tensor that has a gradient (:28-30): draw the
+mask, broadcast the bool mask from rank 0, gather, all-reduce, divide,
+masked_scatter (:32-42).  Here one select+gather kernel runs over the whole
+arena, ONE all-reduce moves the packed values (about p*N elements), one
+scatter kernel writes them back.
 
-Mask sources (RandomIndexSelector(mask_source=...)):
-  "philox" (default) — each element's Bernoulli(p) draw comes from
+Mask sources (RandomIndexSelector(p, mask_source=...), SPARTAStrategy(...,
+mask_source=...)):
+  "torch" (default) — the reference's exact draw,
+      torch.bernoulli(torch.full(shape, p, device=param.device)) per tensor in
+      parameter order (same generator calls, so the same selections and the
+      same global RNG state afterwards), rank 0's masks broadcast as one uint8
+      mask arena.  Bit-identical to the reference given the same generator.
+  "philox" (opt-in fast mode) — each element's Bernoulli(p) draw comes from
       Philox4x32-10 keyed by a per-run seed (rank 0's torch.initial_seed(),
       broadcast once) and the iteration; every rank computes the identical mask
-      in-kernel, so the reference's per-step N-byte mask broadcast disappears.
-      Same distribution as the reference, a different random stream.
-  "torch" — the reference's exact draw, torch.bernoulli(torch.full(shape, p))
-      per tensor on the device in parameter order, rank 0's mask broadcast;
-      bit-identical selections to the reference given the same generator state.
+      in-kernel, so the per-step N-byte mask broadcast and the per-tensor
+      draws disappear.  Same distribution, a DIFFERENT random stream: selections
+      are not the reference's, and the global torch RNG is not consumed.
+      Tensors without a gradient are skipped as in the reference (a skip-range
+      table passed to the kernel).
 The ShuffledSequential / Partitioned selectors are the reference's algorithms
-(torch draws on the device) feeding the mask-mode kernels.
+(the same torch draws on the device) feeding the mask-mode kernels.
 """
 import math
 from typing import Optional, Union
@@ -42,7 +50,7 @@ class IndexSelector:
 
 
 class RandomIndexSelector(IndexSelector):
-    def __init__(self, p, mask_source="philox"):
+    def __init__(self, p, mask_source="torch"):
         super().__init__(p)
         if mask_source not in ("philox", "torch"):
             raise ValueError(f"mask_source must be 'philox' or 'torch', got {mask_source!r}")
@@ -113,6 +121,8 @@ class SparseCommunicator(CommunicationModule):
         self._engine = None
         self._seed = None
         self._mask = None
+        self._skip_key = None
+        self._skip = None
 
     def _init_node(self, model, rank, num_nodes):
         pass
@@ -134,6 +144,24 @@ class SparseCommunicator(CommunicationModule):
             self._seed = int(t.item())
         return self._seed
 
+    def _skip_table(self):
+        """[lo, hi) arena ranges of the tensors that are skipped this step
+        (`not requires_grad or grad is None`, sparta.py:29-30), merged; None
+        when every tensor takes part.  Cached on the device while unchanged."""
+        a = self.strategy.arena
+        key = tuple(i for i, p in enumerate(a.params) if not p.requires_grad or p.grad is None)
+        if key != self._skip_key:
+            rng = []
+            for i in key:
+                lo, hi = a.layout.offsets[i], a.layout.offsets[i] + a.layout.numels[i]
+                if rng and rng[-1][1] == lo:
+                    rng[-1][1] = hi
+                else:
+                    rng.append([lo, hi])
+            self._skip = torch.tensor(rng, dtype=torch.int64, device=a.device).view(-1, 2) if rng else None
+            self._skip_key = key
+        return self._skip
+
     def _build_mask(self, model):
         """Reference mask path: per-tensor selector draws into one uint8 mask
         arena (frozen / grad-less tensors stay 0), then rank 0's is broadcast."""
@@ -150,6 +178,10 @@ class SparseCommunicator(CommunicationModule):
         s.coll.broadcast_(self._mask, 0)
         return self._mask
 
+    def finish(self):
+        if self._engine is not None:
+            self._engine.check()
+
     def communicate(self, model, rank: int, num_nodes: int, local_step: int) -> None:
         if num_nodes > 1:
             if self._engine is None:
@@ -159,7 +191,7 @@ class SparseCommunicator(CommunicationModule):
             with torch.no_grad():
                 reps = s.arena.flat.view(1, -1)
                 if self._philox_mode():
-                    self._engine(reps, seed=self._shared_seed(), iteration=self.iteration)
+                    self._engine(reps, seed=self._shared_seed(), iteration=self.iteration, skip=self._skip_table())
                 else:
                     self._engine(reps, mask=self._build_mask(model))
         self.iteration += 1
@@ -167,7 +199,7 @@ class SparseCommunicator(CommunicationModule):
 
 class SPARTAStrategy(CommunicateOptimizeStrategy):
     def __init__(self, inner_optim: Optional[Union[str, OptimSpec]] = None, p_sparta=0.005,
-                 mask_source="philox", **kwargs):
+                 mask_source="torch", **kwargs):
         index_selector = RandomIndexSelector(p_sparta, mask_source=mask_source)
         sparse_comm = SparseCommunicator(index_selector)
         super().__init__(inner_optim=inner_optim, communication_modules=[sparse_comm], **kwargs)

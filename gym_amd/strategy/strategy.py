@@ -112,6 +112,11 @@ class Strategy(ABC, LogModule):
                     cb(self.scheduler.get_last_lr()[0])
         self.local_step += 1
 
+    def finish(self):
+        """End of training (called by TrainNode.train after the last step):
+        surface any deferred device-side error of the step kernels (SPARTA's
+        capacity flag is read back asynchronously)."""
+
     def zero_grad(self):
         arena = getattr(self, "arena", None)
         if arena is not None and arena.grad_flat is not None:

@@ -204,6 +204,7 @@ class TrainNode(LogModule):
                 self.logger.increment_step()
             if self.num_nodes > 1:
                 dist.barrier()
+        self.strategy.finish()
         self._evaluate()
         return self.model.state_dict()
 

@@ -103,28 +103,32 @@ GA_API uint32_t ga_sparta_threshold(double p);
  * Select the SPARTA index set over an arena of n elements and gather the
  * selected values summed over the K local replicas.
  *   mask source: if mask != null, element i is selected iff mask[i] != 0
- *   (uint8 mask, rank 0's mask broadcast — sparta.py:121-126); otherwise the
- *   in-kernel Philox4x32-10 stream decides: select iff
- *   (philox(key=seed, ctr={i/4, iteration})[i%4] >> 8) < threshold.
+ *   (uint8 mask arena: rank 0's per-tensor index_selector masks, broadcast --
+ *   sparta.py:32-37); otherwise the in-kernel Philox4x32-10 stream decides:
+ *   select iff (philox(key=seed, ctr={i/4, iteration})[i%4] >> 8) < threshold,
+ *   except inside the `nskip` element ranges skip[2r] <= i < skip[2r+1]
+ *   (sorted, disjoint: the tensors without a gradient, which the reference
+ *   skips, sparta.py:29-30; skip may be null when nskip == 0).
  * Outputs (device): idx[j] = j-th selected element index in ascending order
- * (row-major over the arena, == param.data[mask] order, sparta.py:127),
+ * (row-major over the arena, == param.data[mask] order, sparta.py:38),
  * vals[j] = sum_k src_k[idx[j]], count[0] = number selected (int64),
  * count[1] = 1 if that exceeded `cap` (only the first cap are written).
  * `work` must hold ga_sparta_workspace_bytes(n) bytes.
  *
- * Replaces: RandomIndexSelector.get_indices (sparta.py:169-174), the mask
- * broadcast and gather of SparseCommunicator.communicate (sparta.py:113-131).
+ * Replaces: RandomIndexSelector.get_indices (sparta.py:80-85), the mask
+ * broadcast and gather of SparseCommunicator.communicate (sparta.py:24-38).
  */
 GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld,
                             int64_t n, const uint8_t* mask, uint64_t seed,
-                            uint64_t iteration, uint32_t threshold, int64_t cap,
+                            uint64_t iteration, uint32_t threshold,
+                            const int64_t* skip, int64_t nskip, int64_t cap,
                             int32_t* idx, void* vals, int64_t* count, void* work,
                             hipStream_t stream);
 
 /*
  * dst_k[idx[j]] = vals[j] / divisor for j < min(count[0], cap), k < K.
  * Replaces: `sparse_data /= num_nodes; param.masked_scatter_(mask, sparse_data)`
- * (sparta.py:129-131).
+ * (sparta.py:40-42).
  */
 GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
                              const int64_t* count, int64_t cap, float divisor,
@@ -136,11 +140,12 @@ GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
  * <- (sum over the K replicas) / divisor, in the same pass (the gathered lines
  * are written back while still in L2).  idx/vals/count/work may all be null
  * (no packed list, no count/scan pass); if given they are filled as by
- * ga_sparta_select.  Replaces sparta.py:113-131 for batched replicas.
+ * ga_sparta_select.  Replaces sparta.py:24-44 for batched replicas.
  */
 GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
                                    const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                   uint32_t threshold, float divisor, int32_t* idx, void* vals,
+                                   uint32_t threshold, const int64_t* skip, int64_t nskip,
+                                   float divisor, int32_t* idx, void* vals,
                                    int64_t cap, int64_t* count, void* work, hipStream_t stream);
 
 /* ---- DeMo DCT codec ------------------------------------------------------ */

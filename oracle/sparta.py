@@ -1,12 +1,14 @@
 """SPARTA sparse averaging and the selector masks (oracle; test infrastructure only).
 
-Reference: SparseCommunicator.communicate (exogym/strategy/sparta.py:113-131):
-  mask = rank 0's index_selector.get_indices(param, iteration)   (:121-126, broadcast)
-  v = param.data[mask]            row-major order over the tensor (:127)
-  v = (sum_k v_k) / num_nodes     all_reduce SUM then true division (:128-129)
-  param.masked_scatter_(mask, v)  (:131)
+Reference: SparseCommunicator.communicate (exogym/strategy/sparta.py:24-44):
+  mask = rank 0's index_selector.get_indices(param, iteration)   (:32-37, broadcast)
+  v = param.data[mask]            row-major order over the tensor (:38)
+  v = (sum_k v_k) / num_nodes     all_reduce SUM then true division (:39-40)
+  param.masked_scatter_(mask, v)  (:42)
+  tensors with `not requires_grad or grad is None` are skipped (:29-30).
 Selectors restated given their torch random draws as inputs:
-  ShuffledSequentialIndexSelector (:177-225), PartitionedIndexSelector (:228-282).
+  RandomIndexSelector (:80-85), ShuffledSequentialIndexSelector (:88-136),
+  PartitionedIndexSelector (:139-193).
 
 gym_amd's fast mask mode has no reference counterpart: it draws the mask from
 Philox4x32-10 (Salmon et al., SC'11, "Parallel random numbers: as easy as
@@ -55,8 +57,11 @@ def threshold(p):
     return int(math.ceil(p * 16777216.0))
 
 
-def philox_mask(n, seed, iteration, p, start=0):
-    """Mask bits of arena elements [start, start+n) for (seed, iteration)."""
+def philox_mask(n, seed, iteration, p, start=0, skip=None):
+    """Mask bits of arena elements [start, start+n) for (seed, iteration);
+    elements inside a `skip` range [lo, hi) are never selected (tensors
+    without a gradient, which SparseCommunicator.communicate skips,
+    exogym/strategy/sparta.py:29-30)."""
     idx = np.arange(start, start + n, dtype=np.uint64)
     q = idx >> np.uint64(2)
     ctr = np.stack([(q & MASK32).astype(np.uint32), (q >> np.uint64(32)).astype(np.uint32),
@@ -66,12 +71,17 @@ def philox_mask(n, seed, iteration, p, start=0):
     words = philox4x32_10(ctr, key)
     lane = (idx & np.uint64(3)).astype(np.int64)
     w = words[np.arange(n), lane]
-    return (w >> np.uint32(8)) < np.uint32(threshold(p))
+    m = (w >> np.uint32(8)) < np.uint32(threshold(p))
+    for lo, hi in (skip if skip is not None else ()):
+        a, b = max(int(lo) - start, 0), min(int(hi) - start, n)
+        if a < b:
+            m[a:b] = False
+    return m
 
 
 def sparse_average(node_params, mask, divisor=None):
     """node_params: list of K arrays of one tensor; mask: bool array of the same
-    shape.  Returns the K updated arrays (sparta.py:127-131)."""
+    shape.  Returns the K updated arrays (sparta.py:38-42)."""
     flat_mask = np.asarray(mask, dtype=bool).reshape(-1)
     vals = [np.asarray(p, dtype=np.float32).reshape(-1)[flat_mask] for p in node_params]
     avg = mean_reduce(vals, divisor if divisor is not None else len(node_params))
@@ -89,7 +99,7 @@ def selected_indices(mask):
 
 
 def shuffled_sequential_mask(numel, p, shuffled_indices, iteration):
-    """ShuffledSequentialIndexSelector.get_indices (sparta.py:184-225) given the
+    """ShuffledSequentialIndexSelector.get_indices (sparta.py:95-136) given the
     tensor's randperm drawn on first use."""
     if numel == 0:
         return np.zeros(0, dtype=bool)
@@ -104,7 +114,7 @@ def shuffled_sequential_mask(numel, p, shuffled_indices, iteration):
 
 
 def partitioned_masks(numel, p, rank_orders, calls):
-    """PartitionedIndexSelector.get_indices (sparta.py:235-282) for `calls`
+    """PartitionedIndexSelector.get_indices (sparta.py:146-193) for `calls`
     consecutive calls on one tensor, given the orders torch.rand(numel).argsort()
     produced at each (re)partition (rank_orders[j] for the j-th; argsort's order
     among tied draws is torch's, so it is an input here, like the randperm of

@@ -56,8 +56,13 @@ def sparta_workspace(n, device):
     return torch.empty(16, dtype=torch.uint8, device=device)
 
 
-def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0):
-    m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p)
+def _skip_list(skip):
+    return None if skip is None else [tuple(r) for r in skip.cpu().tolist()]
+
+
+def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0, skip=None):
+    m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
+                                                                           skip=_skip_list(skip))
     sel = np.flatnonzero(m)
     count[0] = len(sel)
     count[1] = int(len(sel) > cap)
@@ -76,8 +81,9 @@ def sparta_scatter(vals, idx, count, cap, divisor, dst):
 
 
 def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0, idx=None, vals=None, cap=0,
-                         count=None, work=None):
-    m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p)
+                         count=None, work=None, skip=None):
+    m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
+                                                                           skip=_skip_list(skip))
     r2 = _2d(reps)
     out = osparta.sparse_average(list(_np(r2)[:, :n]), m, divisor)
     for k in range(r2.shape[0]):

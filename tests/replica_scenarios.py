@@ -28,8 +28,10 @@ def make_strategy(name):
         return SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-2), max_norm=1.0)
     if name == "diloco":
         return DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-2), H=2)
-    if name == "sparta":
+    if name == "sparta":  # the reference's torch-drawn masks (default)
         return SPARTAStrategy(inner_optim=OptimSpec(torch.optim.AdamW, lr=1e-2), p_sparta=0.1)
+    if name == "sparta_philox":
+        return SPARTAStrategy(inner_optim=OptimSpec(torch.optim.AdamW, lr=1e-2), p_sparta=0.1, mask_source="philox")
     if name == "fedavg":
         return FedAvgStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.05), H=2, max_norm=0.5)
     if name == "demo":

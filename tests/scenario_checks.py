@@ -58,6 +58,67 @@ def check_sparta_philox(res, world, golden_dir):
             np.testing.assert_allclose(res[r]["after"], reps[r], rtol=1e-6, atol=1e-9)
 
 
+def _torch_masks(kind, device, steps):
+    """Rank 0's masks for `steps` calls, re-derived from the generator calls the
+    reference selectors make (sparta.py:80-85, :95-136, :146-193) on `device`
+    after torch.manual_seed(42), through the oracle's restatements (the draws
+    are inputs, as torch's randperm/argsort order is the generator's)."""
+    import torch
+    import strategy_scenarios as S
+    p = S.SEL_P[kind]
+    live = [i for i in range(len(S.SEL_SHAPES)) if i != S.SEL_FROZEN]
+    numel = {i: int(np.prod(S.SEL_SHAPES[i])) for i in live}
+    torch.manual_seed(42)
+    masks, perms, orders, calls = [], {}, {i: [] for i in live}, 0
+    for it in range(steps):
+        m = {}
+        for i in live:
+            if kind == "random":
+                m[i] = torch.bernoulli(torch.full(S.SEL_SHAPES[i], p, device=device)).bool().cpu().numpy().reshape(-1)
+            elif kind == "shuffled":
+                if i not in perms:
+                    perms[i] = torch.randperm(numel[i], device=device).cpu().numpy()
+                m[i] = osparta.shuffled_sequential_mask(numel[i], p, perms[i], it)
+            else:  # partitioned: a new argsort at the first call and after each full cycle
+                nparts = max(1, min(int(np.ceil(1.0 / p)), numel[i]))
+                if it % nparts == 0:
+                    orders[i].append(torch.rand(numel[i], device=device).argsort().cpu().numpy())
+                m[i] = osparta.partitioned_masks(numel[i], p, orders[i], it + 1)[-1]
+        masks.append(m)
+    return masks
+
+
+def check_sparta_sel(res, world, golden_dir, kind="random", device="cpu"):
+    import strategy_scenarios as S
+    nt = len(S.SEL_SHAPES)
+    if kind == "philox":
+        seed = int(res[0]["seed_0"])
+        offs = res[0]["offsets_0"]
+        n_tot = int(offs[-1]) + int(np.prod(S.SEL_SHAPES[-1]))
+        skip = [(int(offs[S.SEL_FROZEN]), int(offs[S.SEL_FROZEN]) + int(np.prod(S.SEL_SHAPES[S.SEL_FROZEN])))]
+        masks = []
+        for it in range(S.SEL_STEPS):
+            full = osparta.philox_mask(n_tot, seed, it, S.SEL_P[kind], skip=skip)
+            masks.append({i: full[int(offs[i]):int(offs[i]) + int(np.prod(S.SEL_SHAPES[i]))]
+                          for i in range(nt) if i != S.SEL_FROZEN})
+    else:
+        masks = _torch_masks(kind, device, S.SEL_STEPS)
+    for step in range(S.SEL_STEPS):
+        for i in range(nt):
+            before = [res[r][f"before_{step}_{i}"] for r in range(world)]
+            if i == S.SEL_FROZEN:
+                want = before
+            else:
+                assert masks[step][i].any() or kind in ("random", "philox")
+                want = osparta.sparse_average(before, masks[step][i].reshape(S.SEL_SHAPES[i]))
+            for r in range(world):
+                got = res[r][f"after_{step}_{i}"]
+                if world == 2:
+                    assert np.array_equal(got, want[r]), f"{kind} step {step} tensor {i} rank {r}"
+                else:
+                    np.testing.assert_allclose(got, want[r], rtol=1e-6, atol=1e-9)
+
+
 def check_fedavg(res, world, golden_dir, island_size=None):
     nt = 3
     before = [[res[r][f"before_{i}"] for i in range(nt)] for r in range(world)]
@@ -143,4 +204,4 @@ def check_simple_adamw(res, world, golden_dir, steps=3):
 
 
 CHECKS = {"simple_adamw": check_simple_adamw, "engine": check_engine, "simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
-          "sparta_philox": check_sparta_philox, "fedavg": check_fedavg, "demo": check_demo}
+          "sparta_philox": check_sparta_philox, "sparta_sel": check_sparta_sel, "fedavg": check_fedavg, "demo": check_demo}

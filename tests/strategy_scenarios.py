@@ -130,7 +130,7 @@ def sc_sparta_philox(rank, world, dev, golden_dir):
     shapes = [(66, 32), (128,), (96, 64), (3, 7)]
     torch.manual_seed(42)
     model = ShapeModel(shapes, seed=77 + rank).to(dev)
-    s = SPARTAStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.0), p_sparta=0.05)
+    s = SPARTAStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.0), p_sparta=0.05, mask_source="philox")
     s._init_node(model, rank, world)
     out = {"before": _host(s.arena.flat)}
     s.zero_grad()
@@ -141,6 +141,48 @@ def sc_sparta_philox(rank, world, dev, golden_dir):
     out["seed"] = np.array(s.communication_modules[0]._seed, dtype=np.int64)
     out["n"] = np.array(s.arena.n)
     return out
+
+
+SEL_SHAPES = [(66, 32), (128,), (5, 9), (96, 64), (3, 7)]
+SEL_FROZEN = 2  # a requires_grad=False tensor: never averaged (sparta.py:29-30)
+SEL_P = {"random": 0.05, "shuffled": 0.1, "partitioned": 0.25, "philox": 0.05}
+SEL_STEPS = 5
+
+
+def make_selector(kind):
+    from gym_amd.strategy.sparta import (PartitionedIndexSelector, RandomIndexSelector,
+                                         ShuffledSequentialIndexSelector)
+    p = SEL_P[kind]
+    if kind == "shuffled":
+        return ShuffledSequentialIndexSelector(p)
+    if kind == "partitioned":
+        return PartitionedIndexSelector(p)
+    return RandomIndexSelector(p, mask_source="philox" if kind == "philox" else "torch")
+
+
+def sc_sparta_sel(rank, world, dev, golden_dir, kind="random"):
+    """SparseCommunicator with each index selector, driven the way a reference
+    user builds it (CommunicateOptimizeStrategy([SparseCommunicator(sel)])),
+    plus a frozen tensor that must be left alone."""
+    from gym_amd.strategy import CommunicateOptimizeStrategy, OptimSpec
+    from gym_amd.strategy.sparta import SparseCommunicator
+    torch.manual_seed(42)  # TrainNode seeds every rank (train_node.py:50-53)
+    model = ShapeModel(SEL_SHAPES, seed=300 + rank).to(dev)
+    model.ps[SEL_FROZEN].requires_grad_(False)
+    comm = SparseCommunicator(make_selector(kind))
+    s = CommunicateOptimizeStrategy([comm], inner_optim=OptimSpec(torch.optim.SGD, lr=0.0))
+    s._init_node(model, rank, world)
+    out = {}
+    for step in range(SEL_STEPS):
+        out[f"before_{step}"] = [_host(p) for p in model.parameters()]
+        s.zero_grad()
+        s.step()
+        out[f"after_{step}"] = [_host(p) for p in model.parameters()]
+    s.finish()
+    if kind == "philox":
+        out["seed"] = [np.array(comm._seed, dtype=np.int64)]
+        out["offsets"] = [np.array(s.arena.layout.offsets, dtype=np.int64)]
+    return {f"{k}_{i}": v for k, lst in out.items() for i, v in enumerate(lst)}
 
 
 def sc_fedavg(rank, world, dev, golden_dir, island_size=None):
@@ -245,6 +287,7 @@ def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4):
 
 
 SCENARIOS = {"simple_adamw": sc_simple_adamw, "engine": sc_engine, "simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
+             "sparta_sel": sc_sparta_sel,
              "fedavg": sc_fedavg, "demo": sc_demo}
 
 

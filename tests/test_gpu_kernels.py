@@ -241,6 +241,38 @@ def test_sparta_average_local(K, with_list, use_mask):
         assert c == int(m.sum()) and np.array_equal(idx[:c].cpu().numpy(), np.flatnonzero(m))
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_sparta_philox_skip_ranges(fused):
+    """Tensors without a gradient are never selected (sparta.py:29-30): skip
+    ranges that start/end inside a 16-element group, adjacent ranges, one
+    covering whole tiles, one at the arena end."""
+    from gym_amd import ops
+    n, p, K = 200_003, 0.2, 2
+    skip = [(0, 5), (5, 17), (33, 34), (1000, 9192), (12_301, 12_302), (50_000, 150_000), (199_990, 200_003)]
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    seed, it = 0xABCDEF, 3
+    m = osparta.philox_mask(n, seed, it, p, skip=skip)
+    assert not any(m[a:b].any() for a, b in skip) and m.sum() > 0
+    cap = int(m.sum()) + 16
+    idx, count, work = _sparta_buffers(n, cap)
+    vals = torch.empty(cap, device=DEV)
+    sk = torch.tensor(skip, dtype=torch.int64, device=DEV)
+    src = t(x)
+    if fused:
+        ops.sparta_average_local(src, n, float(K), seed=seed, iteration=it, p=p, idx=idx, vals=vals, cap=cap,
+                                 count=count, work=work, skip=sk)
+    else:
+        ops.sparta_select(src, n, cap, idx, vals, count, work, seed=seed, iteration=it, p=p, skip=sk)
+        ops.sparta_scatter(vals, idx, count, cap, float(K), src)
+    c = int(count[0].item())
+    assert c == int(m.sum()) and np.array_equal(idx[:c].cpu().numpy(), np.flatnonzero(m))
+    want = osparta.sparse_average(list(x), m)
+    got = host(src)
+    for k in range(K):
+        assert np.array_equal(got[k], want[k])
+
+
 def test_sparta_overflow_flag():
     from gym_amd import ops
     n = 10_000

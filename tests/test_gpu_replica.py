@@ -9,7 +9,7 @@ import replica_scenarios as R
 
 pytestmark = pytest.mark.gpu
 
-NAMES = ["simple", "diloco", "sparta", "fedavg", "demo"]
+NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "demo"]
 
 
 @pytest.mark.parametrize("name", NAMES)

@@ -19,6 +19,9 @@ CASES = [
     ("engine", 3, {}),
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": True}),
     ("sparta_philox", 2, {}),
+    ("sparta_sel", 2, {"kind": "random"}), ("sparta_sel", 3, {"kind": "random"}),
+    ("sparta_sel", 2, {"kind": "shuffled"}), ("sparta_sel", 2, {"kind": "partitioned"}),
+    ("sparta_sel", 3, {"kind": "philox"}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),
     ("demo", 2, {}),
 ]
@@ -29,5 +32,7 @@ def test_strategy_on_gpu(tmp_path, name, world, kw):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = S.run(name, world, "cuda:0", False, str(tmp_path), GOLDEN, **kw)
-    check_kw = {"island_size": kw["island_size"]} if "island_size" in kw else {}
+    check_kw = {k: kw[k] for k in ("island_size", "kind") if k in kw}
+    if name == "sparta_sel":
+        check_kw["device"] = "cuda:0"
     CHECKS[name](res, world, GOLDEN, **check_kw)

@@ -6,7 +6,7 @@ import pytest
 
 import replica_scenarios as R
 
-NAMES = ["simple", "diloco", "sparta", "fedavg", "demo"]
+NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "demo"]
 
 
 @pytest.fixture
@@ -42,6 +42,7 @@ def test_replica_layout_rules():
     assert replica_layout(6, [0, 1, 2, 3], "auto", s) is None          # not a multiple: gloo path
     assert replica_layout(8, [0, 1], 4, s) == (2, 4)
     assert replica_layout(8, [0, 1], 1, s) is None
-    assert replica_layout(8, [0], "auto", SPARTAStrategy(mask_source="torch")) is None
+    assert replica_layout(8, [0], "auto", SPARTAStrategy()) == (1, 8)  # torch-drawn masks batch too
+    assert replica_layout(8, [0], "auto", SPARTAStrategy(mask_source="philox")) == (1, 8)
     with pytest.raises(ValueError):
         replica_layout(8, [0], 4, s)  # 2 processes on 1 GPU

@@ -16,6 +16,9 @@ CASES = [
     ("engine", 3, {}), ("engine", 2, {"chunks": 1}),
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": False}),
     ("sparta_philox", 2, {}),
+    ("sparta_sel", 2, {"kind": "random"}), ("sparta_sel", 3, {"kind": "random"}),
+    ("sparta_sel", 2, {"kind": "shuffled"}), ("sparta_sel", 2, {"kind": "partitioned"}),
+    ("sparta_sel", 3, {"kind": "philox"}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),
     ("demo", 2, {}),
 ]
@@ -24,5 +27,7 @@ CASES = [
 @pytest.mark.parametrize("name,world,kw", CASES, ids=[f"{c[0]}-w{c[1]}-{c[2]}" for c in CASES])
 def test_strategy_orchestration_gloo(tmp_path, name, world, kw):
     res = S.run(name, world, "cpu", True, str(tmp_path), GOLDEN, **kw)
-    check_kw = {"island_size": kw["island_size"]} if "island_size" in kw else {}
+    check_kw = {k: kw[k] for k in ("island_size", "kind") if k in kw}
+    if name == "sparta_sel":
+        check_kw["device"] = "cpu"
     CHECKS[name](res, world, GOLDEN, **check_kw)
