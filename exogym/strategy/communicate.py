@@ -1,0 +1,7 @@
+"""exogym.strategy.communicate -> gym_amd.strategy.communicate (the same module object: attribute look-ups,
+monkeypatching and isinstance checks see gym_amd's implementation)."""
+import sys
+
+from gym_amd.strategy import communicate as _impl
+
+sys.modules[__name__] = _impl

@@ -1,0 +1,7 @@
+"""exogym.trainer -> gym_amd.trainer (the same module object: attribute look-ups,
+monkeypatching and isinstance checks see gym_amd's implementation)."""
+import sys
+
+from gym_amd import trainer as _impl
+
+sys.modules[__name__] = _impl

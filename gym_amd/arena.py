@@ -3,7 +3,7 @@
 One simulated node's parameters live in ONE contiguous buffer so a single
 kernel launch (and a single RCCL call) covers every tensor, instead of the
 reference's per-tensor loops (e.g. strategy.py:130-133, diloco.py:34-41,
-sparta.py:117-131).  Tensor offsets are aligned to 64 elements (256 B for
+sparta.py:28-42).  Tensor offsets are aligned to 64 elements (256 B for
 fp32) so every tensor starts on a cache line and 16-byte vector loads stay
 aligned; the padding between tensors is kept at zero, so elementwise kernels
 may run over the whole arena.

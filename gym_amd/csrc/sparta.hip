@@ -4,7 +4,7 @@
 //
 // Selection is a stream compaction in ascending element order, so the packed
 // order equals `param.data[mask]` over the concatenated parameters
-// (sparta.py:127).  The mask is either a uint8 arena (rank 0's mask, exactly
+// (sparta.py:38).  The mask is either a uint8 arena (rank 0's mask, exactly
 // the reference semantics) or generated in-kernel by Philox4x32-10 keyed by
 // (seed, iteration) — then every rank derives the same mask and nothing is
 // broadcast.  Three passes: per-tile count, one-block scan of tile counts,

@@ -26,6 +26,7 @@ import torch.distributed as dist
 
 from ...arena import ParamArena
 from ...comm import Collective
+from ...demo_codec import smaller_split as _get_smaller_split  # noqa: F401  (demo.py:489-498, same name)
 from ...engine import DeMoCodec
 
 _REQUIRE_GPU = True  # the CPU orchestration tests swap the kernels for oracle stand-ins

@@ -9,9 +9,9 @@ local_step % H == 0 and local_step > 0.
 Full averaging is one RCCL all-reduce over the parameter arena plus one
 division kernel (the reference: a per-tensor all-reduce + divide).  Island
 averaging keeps the reference's algorithm — rank 0 shuffles the ranks with
-Python's `random` and broadcasts the permutation (:308-333), every node
+Python's `random` and broadcasts the permutation (:27-51), every node
 all-gathers the parameters and averages its island's members in ascending
-rank order (:343-351) — as ONE all-gather of the arena and one
+rank order (:61-69) — as ONE all-gather of the arena and one
 ga_replica_mean over the member rows.
 """
 import random

@@ -16,7 +16,7 @@ published Philox4x32-10 known-answer vectors instead.
 Modules:
   reduce    mean over nodes                 strategy.py:130-133, diloco.py:34-37
   diloco    fused outer SGD/Nesterov step   diloco.py:43-76 + torch sgd.py
-  sparta    masked gather/average/scatter   sparta.py:113-131; Philox4x32-10 mask
+  sparta    masked gather/average/scatter   sparta.py:24-44; Philox4x32-10 mask
   demo      DCT codec + DeMo step           demo_impl/demo.py:142-498
   schedule  lambda_cosine LR                strategy.py:65-95
 """

@@ -9,8 +9,8 @@ Each fixture exercises the reference's own code on CPU/gloo with small seeded
 inputs:
   mean_reduce.npz   G1  communicate.all_reduce + div_  (strategy.py:130-133), K in {2,3,8}
   diloco.npz        G2  DiLoCoStrategy outer steps (diloco.py:51-76), K=3, H=2, 3 outer steps
-  sparta.npz        G3  SPARTAStrategy communicate (sparta.py:113-131), K=2 and K=3, masks logged
-  sparta_sel.npz    G3b ShuffledSequential / Partitioned selector masks (sparta.py:177-282)
+  sparta.npz        G3  SPARTAStrategy communicate (sparta.py:24-44), K=2 and K=3, masks logged
+  sparta_sel.npz    G3b ShuffledSequential / Partitioned selector masks (sparta.py:88-193)
   demo_codec.npz    G4  _dct/_idct bases, _get_smaller_split, TransformDCT encode/decode,
                         CompressDCT compress/decompress/batch_decompress (demo_impl/demo.py)
   demo_steps.npz    G4  3 full DeMo.step()s with K=2 over gloo (demo.py:142-209)
@@ -222,7 +222,7 @@ def g3_worker(rank, world, port, q):
         rec[f"before_{call}"] = [p.detach().numpy().copy() for p in model.parameters()]
         strat.step()
         rec[f"after_{call}"] = [p.detach().numpy().copy() for p in model.parameters()]
-        # the mask actually used is rank 0's (broadcast, sparta.py:126); log what rank 0 drew
+        # the mask actually used is rank 0's (broadcast, sparta.py:37); log what rank 0 drew
         rec[f"mask_{call}"] = [m.numpy().copy() for m in masks]
     q.put((rank, rec))
     dist.destroy_process_group()
