@@ -41,6 +41,18 @@ class ArenaLayout:
     def __len__(self):
         return len(self.shapes)
 
+    def subset(self, indices):
+        """The tensors `indices` of this layout at their offsets in the SAME
+        arena (n unchanged): e.g. the trainable tensors a codec covers while
+        frozen ones stay in the arena untouched."""
+        sub = object.__new__(ArenaLayout)
+        sub.shapes = [self.shapes[i] for i in indices]
+        sub.numels = [self.numels[i] for i in indices]
+        sub.offsets = [self.offsets[i] for i in indices]
+        sub.n_params = sum(sub.numels)
+        sub.n = self.n
+        return sub
+
     def views(self, flat):
         """Per-tensor views of a flat [>= n] buffer."""
         return [flat[o:o + n].view(s) for o, n, s in zip(self.offsets, self.numels, self.shapes)]

@@ -13,7 +13,9 @@ step kernel applies on the device -- no host synchronisation.
 Exactness: parameters whose .grad is None at step time are skipped, as torch
 does (the kernel runs over the contiguous arena ranges that have gradients).
 The per-parameter state (exp_avg, exp_avg_sq, step) are views of the flat
-state buffers, so state_dict() has torch's layout.
+state buffers, so state_dict() has torch's layout, and load_state_dict()
+(of an ArenaAdam or a torch.optim.Adam/AdamW state dict) copies the loaded
+moments into those buffers, so a resumed run continues where it stopped.
 """
 import math
 
@@ -81,17 +83,47 @@ class ArenaAdam(torch.optim.Optimizer):
             for i, p in enumerate(ar.params):
                 where[id(p)] = (k, ar.layout.offsets[i], ar.layout.numels[i])
         self._spans = [[] for _ in self.arenas]  # per replica: (param, offset, numel) in arena order
+        self._where = where
         for p in self.param_groups[0]["params"]:
             if id(p) not in where:
                 raise ValueError("ArenaAdam: every parameter must live in the arena")
             k, o, n = where[id(p)]
             self._spans[k].append((p, o, n))
-            self.state[p] = {"step": self._step_t, "exp_avg": self.M[k, o:o + n].view(p.shape),
-                             "exp_avg_sq": self.V[k, o:o + n].view(p.shape)}
+            self._bind_state(p)
         for sp in self._spans:
             sp.sort(key=lambda t: t[1])
         self._partials = ops.sumsq_partials(dev, self.K)
         self._clip = torch.ones(2 * self.K, dtype=torch.float32, device=dev)
+
+    def _bind_state(self, p):
+        k, o, n = self._where[id(p)]
+        self.state[p] = {"step": self._step_t, "exp_avg": self.M[k, o:o + n].view(p.shape),
+                         "exp_avg_sq": self.V[k, o:o + n].view(p.shape)}
+
+    def load_state_dict(self, state_dict):
+        """torch's Optimizer.load_state_dict, then the loaded per-parameter
+        moments are copied into the flat state buffers the kernel reads and the
+        state is re-pointed at those views.  The kernel keeps one step count
+        for the arena, so every parameter must carry the same `step`."""
+        super().load_state_dict(state_dict)
+        steps = set()
+        with torch.no_grad():
+            self.M.zero_()
+            self.V.zero_()
+            for p in self.param_groups[0]["params"]:
+                st = self.state.get(p, {})
+                k, o, n = self._where[id(p)]
+                if "exp_avg" in st:
+                    self.M[k, o:o + n].copy_(st["exp_avg"].reshape(-1))
+                    self.V[k, o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                if "step" in st:
+                    steps.add(float(st["step"]))
+        if len(steps) > 1:
+            raise ValueError(f"ArenaAdam: parameters carry different step counts {sorted(steps)}; "
+                             "the fused step keeps one count per arena")
+        self._step_t = torch.tensor(steps.pop() if steps else 0.0)
+        for p in self.param_groups[0]["params"]:
+            self._bind_state(p)
 
     def _ranges(self, k):
         """Contiguous ranges [a, b) of replica k's arena whose parameters have a

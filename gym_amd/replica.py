@@ -103,10 +103,14 @@ class ReplicaRunner:
         self.max_norm = None
         self.lr_scheds = []
         if isinstance(s, DeMoStrategy):
-            self.optim = _LRGroup(s.kwargs.get("lr", 0.001))
+            kw = s.optimizer_kwargs()
+            self.demo_kw = kw
+            self.optim = _LRGroup(kw.get("lr", 0.001))
             self.delta = torch.zeros_like(self.ra.flat_set)
-            self.codec = DeMoCodec(self.coll, self.K, self.ra.layout, dev, chunk=s.compression_chunk,
-                                   topk=s.compression_topk)
+            # the codec covers the trainable tensors only, as DeMo's param list (demo.py:99-117)
+            live = [i for i, p in enumerate(self.ra.arenas[0].params) if p.requires_grad]
+            self.codec = DeMoCodec(self.coll, self.K, self.ra.layout.subset(live), dev,
+                                   chunk=kw["compression_chunk"], topk=kw["compression_topk"])
         else:
             spec = s.optim_spec if isinstance(s, SimpleReduceStrategy) else s.inner_optim_spec
             if fusable(spec.cls, spec.kwargs, self.ra):
@@ -152,7 +156,8 @@ class ReplicaRunner:
         if isinstance(s, DeMoStrategy):
             self.ra.sync_grads()
             lr = self.optim.param_groups[0]["lr"]
-            self.codec(P, G, self.delta, lr, s.compression_decay, s.weight_decay)
+            kw = self.demo_kw
+            self.codec(P, G, self.delta, lr, kw["compression_decay"], kw["weight_decay"])
         elif isinstance(s, SimpleReduceStrategy):
             self.ra.sync_grads()
             self.mean(G)

@@ -20,8 +20,9 @@ class DeMoStrategy(Strategy):
         self.compression_chunk = compression_chunk
         self.weight_decay = weight_decay
 
-    def _init_node(self, model, rank, num_nodes):
-        super()._init_node(model, rank, num_nodes)
+    def optimizer_kwargs(self):
+        """DeMo's constructor kwargs as the reference builds them (demo.py:31-46),
+        strategy_config.optimizer_kwargs applied last."""
         kw = {
             "compression_decay": self.compression_decay,
             "compression_topk": self.compression_topk,
@@ -32,7 +33,11 @@ class DeMoStrategy(Strategy):
         }
         if hasattr(self, "strategy_config") and hasattr(self.strategy_config, "optimizer_kwargs"):
             kw.update(self.strategy_config.optimizer_kwargs)
-        self.optim = DeMo(model.parameters(), **kw)
+        return kw
+
+    def _init_node(self, model, rank, num_nodes):
+        super()._init_node(model, rank, num_nodes)
+        self.optim = DeMo(model.parameters(), **self.optimizer_kwargs())
         self.arena = self.optim.arena  # zero_grad() zeroes the gradient arena in place
         self.coll = self.optim.coll
         self._setup_scheduler()

@@ -162,6 +162,7 @@ class Trainer:
         for _ in range(num_nodes):
             r, sd = queue.get()
             states[r] = sd
+        self.node_states = [states[r] for r in sorted(states)]  # every node's final state (CPU), node order
         avg = _average_model_states(states)
         if avg is None:
             return None

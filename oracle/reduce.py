@@ -18,3 +18,19 @@ def mean_reduce(node_arrays, divisor=None, rows=None):
         acc = (acc + np.asarray(x, dtype=np.float32)).astype(np.float32)
     d = np.float32(len(xs) if divisor is None else divisor)
     return (acc / d).astype(np.float32)
+
+
+def average_state_dicts(states):
+    """Trainer._average_model_states (exogym/trainer.py:95-119): per entry, the
+    mean over nodes (node order of `states`); floating entries sum in ascending
+    node order then divide by K; integer entries (e.g. BatchNorm's
+    num_batches_tracked) are averaged in float32 and cast back (truncation, as
+    torch's `.to(int)`).  states: list of {name: ndarray}."""
+    out = {}
+    for name in states[0]:
+        xs = [np.asarray(s[name]) for s in states]
+        if np.issubdtype(xs[0].dtype, np.floating):
+            out[name] = mean_reduce(xs).astype(xs[0].dtype)
+        else:
+            out[name] = mean_reduce([x.astype(np.float32) for x in xs]).astype(xs[0].dtype)
+    return out

@@ -191,9 +191,11 @@ def install(monkeypatch_target_modules=None):
     import gym_amd.strategy.diloco as diloco
     import gym_amd.strategy.federated_averaging as fedavg
     import gym_amd.strategy.strategy as strategy
+    import gym_amd.train_node as train_node
+    import gym_amd.trainer as trainer
     import sys
     me = sys.modules[__name__]
-    for mod in (engine, diloco, fedavg, fused_optim, replica):
+    for mod in (engine, diloco, fedavg, fused_optim, replica, train_node, trainer):
         mod.ops = me
     strategy.require_gpu = lambda device: None
     import gym_amd.strategy.demo_impl.demo as demo_mod

@@ -21,7 +21,18 @@ SHAPES = [(66, 32), (128,), (96, 64), (3, 7)]
 STEPS = 4
 
 
+FROZEN = 2  # "<name>_frozen" scenarios freeze this tensor on every node
+
+
+def _model(name, dev):
+    m = ShapeModel(SHAPES, seed=5).to(dev)
+    if name.endswith("_frozen"):
+        m.ps[FROZEN].requires_grad_(False)
+    return m
+
+
 def make_strategy(name):
+    name = name.removesuffix("_frozen")
     from gym_amd.strategy import (DeMoStrategy, DiLoCoStrategy, FedAvgStrategy, OptimSpec, SimpleReduceStrategy,
                                   SPARTAStrategy)
     if name == "simple":
@@ -47,7 +58,8 @@ def node_grads(node, step):
 def _set_grads(model, node, step, dev):
     with torch.no_grad():
         for p, g in zip(model.parameters(), node_grads(node, step)):
-            p.grad.copy_(g.to(dev))
+            if p.requires_grad:
+                p.grad.copy_(g.to(dev))
 
 
 def _proc_worker(rank, world, port, name, device, fake, out_dir):
@@ -61,7 +73,7 @@ def _proc_worker(rank, world, port, name, device, fake, out_dir):
     try:
         torch.manual_seed(42)
         dev = torch.device(device)
-        model = ShapeModel(SHAPES, seed=5).to(dev)
+        model = _model(name, dev)
         s = make_strategy(name)
         s._init_node(model, rank, world)
         for t in range(STEPS):
@@ -89,7 +101,7 @@ def run_replica_mode(name, K, device, fake):
     from gym_amd.replica import ReplicaRunner
     torch.manual_seed(42)
     dev = torch.device(device)
-    models = [ShapeModel(SHAPES, seed=5).to(dev) for _ in range(K)]
+    models = [_model(name, dev) for _ in range(K)]
     runner = ReplicaRunner(make_strategy(name), models, rank=0, num_nodes=K)
     for t in range(STEPS):
         runner.zero_grad()
@@ -104,3 +116,20 @@ def compare(proc, rep, rtol=1e-5, atol=2e-6):
     for node, (a, b) in enumerate(zip(proc, rep)):
         for i, (x, y) in enumerate(zip(a, b)):
             np.testing.assert_allclose(y, x, rtol=rtol, atol=atol, err_msg=f"node {node} tensor {i}")
+
+
+def replica_eval_average(K, device, fake):
+    """ReplicaRunner.averaged_flat (the evaluation's node-averaged model,
+    exogym/train_node.py:183-189, for the K local nodes) after one DiLoCo inner
+    step (the nodes differ): returns (average, per-node arenas)."""
+    from gym_amd.replica import ReplicaRunner
+    torch.manual_seed(42)
+    dev = torch.device(device)
+    models = [ShapeModel(SHAPES, seed=5).to(dev) for _ in range(K)]
+    runner = ReplicaRunner(make_strategy("diloco"), models, rank=0, num_nodes=K)
+    runner.zero_grad()
+    for k, m in enumerate(models):
+        _set_grads(m, k, 0, dev)
+    runner.step()
+    avg = runner.averaged_flat()
+    return avg.float().cpu().numpy(), runner.ra.flat_set.float().cpu().numpy()

@@ -119,6 +119,19 @@ def check_sparta_sel(res, world, golden_dir, kind="random", device="cpu"):
                     np.testing.assert_allclose(got, want[r], rtol=1e-6, atol=1e-9)
 
 
+def check_eval_avg(res, world, golden_dir):
+    for i in range(3):
+        own = [res[r][f"own_{i}"] for r in range(world)]
+        want = oreduce.mean_reduce(own)
+        for r in range(world):
+            assert np.array_equal(res[r][f"after_{i}"], own[r])  # the node's model is not touched
+            if world == 2:
+                assert np.array_equal(res[r][f"avg_{i}"], want)
+            else:  # gloo's ring order: a few ulp of the summands where they cancel
+                scale = max(np.abs(x).max() for x in own)
+                np.testing.assert_allclose(res[r][f"avg_{i}"], want, rtol=1e-6, atol=1e-7 * scale)
+
+
 def check_fedavg(res, world, golden_dir, island_size=None):
     nt = 3
     before = [[res[r][f"before_{i}"] for i in range(nt)] for r in range(world)]
@@ -204,4 +217,5 @@ def check_simple_adamw(res, world, golden_dir, steps=3):
 
 
 CHECKS = {"simple_adamw": check_simple_adamw, "engine": check_engine, "simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
-          "sparta_philox": check_sparta_philox, "sparta_sel": check_sparta_sel, "fedavg": check_fedavg, "demo": check_demo}
+          "sparta_philox": check_sparta_philox, "sparta_sel": check_sparta_sel,
+          "eval_avg": check_eval_avg, "fedavg": check_fedavg, "demo": check_demo}

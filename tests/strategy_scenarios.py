@@ -185,6 +185,29 @@ def sc_sparta_sel(rank, world, dev, golden_dir, kind="random"):
     return {f"{k}_{i}": v for k, lst in out.items() for i, v in enumerate(lst)}
 
 
+def sc_eval_avg(rank, world, dev, golden_dir):
+    """TrainNode._averaged_model (the evaluation's node-averaged clone,
+    exogym/train_node.py:183-189) over the strategy's arena: the clone holds
+    the mean of every node's parameters; the node's own model is untouched."""
+    import tiny_models
+    from gym_amd.strategy import OptimSpec, SimpleReduceStrategy
+    from gym_amd.train_node import TrainNode
+    model = ShapeModel([(66, 32), (128,), (3, 7)], seed=600 + rank).to(dev)
+    s = SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.SGD, lr=0.0))
+    s._init_node(model, rank, world)
+    ds = tiny_models.dataset(n=64)
+    node = TrainNode(model, ds, None, ds, s, dev, rank, world, num_epochs=1, max_steps=1)
+    g = torch.Generator().manual_seed(700 + rank)
+    with torch.no_grad():  # the constructor broadcast rank 0's parameters: make the nodes differ again
+        for p in model.parameters():
+            p.add_((torch.randn(p.shape, generator=g) * 0.1).to(dev))
+    before = [_host(p) for p in model.parameters()]
+    clone = node._averaged_model()
+    return {**{f"own_{i}": v for i, v in enumerate(before)},
+            **{f"avg_{i}": _host(p) for i, p in enumerate(clone.parameters())},
+            **{f"after_{i}": _host(p) for i, p in enumerate(model.parameters())}}
+
+
 def sc_fedavg(rank, world, dev, golden_dir, island_size=None):
     from gym_amd.strategy import FedAvgStrategy, OptimSpec
     shapes = [(66, 32), (128,), (3, 7)]
@@ -287,7 +310,7 @@ def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4):
 
 
 SCENARIOS = {"simple_adamw": sc_simple_adamw, "engine": sc_engine, "simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
-             "sparta_sel": sc_sparta_sel,
+             "sparta_sel": sc_sparta_sel, "eval_avg": sc_eval_avg,
              "fedavg": sc_fedavg, "demo": sc_demo}
 
 

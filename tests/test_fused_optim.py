@@ -49,3 +49,45 @@ def test_oracle_clip_pinned_to_torch():
     assert abs(tot - float(total)) <= 1e-6 * float(total)
     for t, g in zip(ts, gs):
         np.testing.assert_allclose(t.grad.numpy(), (g * np.float32(coef)).astype(np.float32), rtol=1e-6)
+
+
+@pytest.mark.parametrize("source", ["arena", "torch"])
+def test_arena_adam_state_dict_round_trip(fake, source):
+    """Resume: 3 steps, save, load into a fresh optimizer, 2 more steps ==
+    torch.optim.AdamW for 5 steps (the moments and the step count survive)."""
+    import copy
+    from gym_amd.arena import ParamArena
+    from gym_amd.fused_optim import ArenaAdam
+    kw = {"lr": 3e-3, "weight_decay": 0.1}
+    ref_m = C.make_model("cpu")
+    ref = torch.optim.AdamW(ref_m.parameters(), **kw)
+    a = C.make_model("cpu")
+    arena = ParamArena(list(a.parameters()))
+    opt = ArenaAdam(a.parameters(), arena, **kw)
+    for step in range(5):
+        gs = C.grads_for(step)
+        for p, g in zip(ref_m.parameters(), gs):
+            p.grad = g.clone()
+        ref.step()
+        if step == 3:  # resume before step 3 from a saved state
+            saved = copy.deepcopy(opt.state_dict() if source == "arena" else ref_state)
+            params = [p.detach().clone() for p in (a.parameters() if source == "arena" else ref_params)]
+            a = C.make_model("cpu", seed=99)
+            with torch.no_grad():
+                for p, v in zip(a.parameters(), params):
+                    p.copy_(v)
+            arena = ParamArena(list(a.parameters()))
+            opt = ArenaAdam(a.parameters(), arena, **kw)
+            opt.load_state_dict(saved)
+            assert float(opt.state[next(a.parameters())]["step"]) == 3.0
+        arena.zero_grad()
+        for p, g in zip(a.parameters(), gs):
+            p.grad.copy_(g)
+        opt.step()
+        if step == 2:
+            ref_state = copy.deepcopy(ref.state_dict())
+            ref_params = [p.detach().clone() for p in ref_m.parameters()]
+    C.assert_close([p.detach().numpy() for p in a.parameters()], [p.detach().numpy() for p in ref_m.parameters()])
+    # the state the optimizer reports is the state the kernel uses
+    p0 = next(a.parameters())
+    assert opt.state[p0]["exp_avg"].data_ptr() == opt.M.data_ptr()

@@ -2,11 +2,12 @@
 strategies, on CPU with the oracle-backed kernel stand-ins (host logic: arena
 rows, engines over K local nodes, per-node clipping, fused optimizer over the
 replica set, gating); tests/test_gpu_replica.py runs the same with the kernels."""
+import numpy as np
 import pytest
 
 import replica_scenarios as R
 
-NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "demo"]
+NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "demo", "demo_frozen", "sparta_frozen"]
 
 
 @pytest.fixture
@@ -46,3 +47,10 @@ def test_replica_layout_rules():
     assert replica_layout(8, [0], "auto", SPARTAStrategy(mask_source="philox")) == (1, 8)
     with pytest.raises(ValueError):
         replica_layout(8, [0], 4, s)  # 2 processes on 1 GPU
+
+
+def test_replica_eval_average(fake):
+    from oracle.reduce import mean_reduce
+    avg, rows = R.replica_eval_average(3, "cpu", True)
+    assert not np.array_equal(rows[0], rows[1])
+    assert np.array_equal(avg, mean_reduce(list(rows)))

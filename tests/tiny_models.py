@@ -22,3 +22,19 @@ def dataset(n=256, d_in=32, n_cls=4, seed=0):
     w = torch.randn(d_in, n_cls, generator=g)
     y = (x @ w).argmax(dim=1)
     return torch.utils.data.TensorDataset(x, y)
+
+
+class TinyBN(torch.nn.Module):
+    """An MLP with BatchNorm: float running stats plus the int64
+    num_batches_tracked buffer in its state_dict (final averaging must handle
+    both, exogym/trainer.py:95-119)."""
+
+    def __init__(self, d_in=32, d_hidden=64, n_cls=4):
+        super().__init__()
+        self.fc1 = torch.nn.Linear(d_in, d_hidden)
+        self.bn = torch.nn.BatchNorm1d(d_hidden)
+        self.fc2 = torch.nn.Linear(d_hidden, n_cls)
+
+    def forward(self, batch):
+        x, y = batch
+        return torch.nn.functional.cross_entropy(self.fc2(torch.relu(self.bn(self.fc1(x)))), y)
