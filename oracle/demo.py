@@ -148,15 +148,19 @@ def entries(shape, chunk, topk):
     return (R // n1) * (C // n2) * max(1, min(topk, n1 * n2))
 
 
-def demo_step(p, deltas, grads, lr, decay=0.999, topk=32, chunk=64, weight_decay=0.0):
+def demo_step(p, deltas, grads, lr, decay=0.999, topk=32, chunk=64, weight_decay=0.0, detail=False):
     """One DeMo.step for one tensor over K nodes (params identical across nodes).
-    Returns (p_new, [delta_new_k], sign_grad, [(idx_k, val_k)])."""
+    Returns (p_new, [delta_new_k], sign_grad, [(idx_k, val_k)]); with
+    detail=True also (decoded_grad, [(per-chunk k-th margin, max |coefficient|)
+    of node k]) -- the
+    value whose sign is applied and how far each node's top-k set is from a
+    tie (test infrastructure decides where a sign is unambiguous from these)."""
     shape = np.shape(p)
     p64 = np.asarray(p, dtype=np.float64)
     if weight_decay != 0.0:
         p64 = p64 * np.float64(np.float32(1.0 - lr * weight_decay))
     R, C, n1, n2 = tensor_view(shape, chunk)
-    new_deltas, sent = [], []
+    new_deltas, sent, margins = [], [], []
     for d, g in zip(deltas, grads):
         d64 = np.asarray(d, dtype=np.float64)
         if decay != 1:
@@ -164,12 +168,16 @@ def demo_step(p, deltas, grads, lr, decay=0.999, topk=32, chunk=64, weight_decay
         d64 = d64 + lr * np.asarray(g, dtype=np.float64)
         Y = encode(d64, shape, chunk)
         idx, val = topk_chunks(Y, topk)
+        if detail:
+            margins.append((kth_margin(Y, topk), np.abs(Y).max()))
         tx = decode(scatter_mean([idx], [val], n1, n2), shape, chunk)
         new_deltas.append(d64 - tx)
         sent.append((idx, val))
     S = scatter_mean([s[0] for s in sent], [s[1] for s in sent], n1, n2)
     g = decode(S, shape, chunk)
     sgn = np.sign(g)
+    if detail:
+        return p64 - lr * sgn, new_deltas, sgn, sent, g, margins
     return p64 - lr * sgn, new_deltas, sgn, sent
 
 

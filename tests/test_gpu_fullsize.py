@@ -17,6 +17,7 @@ import torch
 from oracle import demo as odemo
 from oracle import diloco as odiloco
 from oracle import sparta as osparta
+import demo_checks
 
 pytestmark = pytest.mark.gpu
 
@@ -123,6 +124,7 @@ def test_demo_gpt2_350m_sampled_chunks():
     e0 = 0
     checked = 0
     kinds = set()
+    tally = demo_checks.SignTally()
     for ti, (shape, off, nel) in enumerate(zip(L.shapes, L.offsets, L.numels)):
         ne = plan.entries_per_tensor[ti]
         R, C, n1, n2 = odemo.tensor_view(shape, 64)
@@ -153,11 +155,12 @@ def test_demo_gpt2_350m_sampled_chunks():
                 # decode of the own payload: p -= lr * sign(IDCT(top-k)), grad = the sign
                 sg = np.sign(R_)
                 gs = gS[off:off + nel].reshape(R, C)[y * n1:(y + 1) * n1, xx * n2:(xx + 1) * n2]
+                tally.check(gs, sg, np.abs(R_) > 1e-5 * np.abs(R_).max(), what=f"{shape} chunk {y},{xx}")
                 ok = gs == sg
-                assert ok.mean() > 0.995
                 p0 = P0[off:off + nel].reshape(R, C)[y * n1:(y + 1) * n1, xx * n2:(xx + 1) * n2]
                 pg = gP[off:off + nel].reshape(R, C)[y * n1:(y + 1) * n1, xx * n2:(xx + 1) * n2]
                 np.testing.assert_allclose(pg[ok], (p0 - np.float32(lr) * sg)[ok], rtol=0, atol=1e-7)
                 checked += 1
         e0 += ne
     assert checked > 50
+    tally.done()

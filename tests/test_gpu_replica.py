@@ -18,11 +18,10 @@ def test_replicas_match_process_per_node_gpu(tmp_path, name):
         pytest.skip("no GPU")
     proc = R.run_process_mode(name, 3, "cuda:0", False, str(tmp_path))
     rep = R.run_replica_mode(name, 3, "cuda:0", False)
-    if name.startswith("demo"):  # decoded signs may flip where the decoded value is ~0 (reordered MFMA sums)
-        import numpy as np
-        for a, b in zip(proc, rep):
-            for x, y in zip(a, b):
-                assert (np.abs(x - y) <= 2e-6 + 1e-5 * np.abs(x)).mean() > 0.995
+    if name.startswith("demo"):
+        # the same kernels on the same payloads (node order), one launch for K
+        # replicas or K launches of one: identical bits
+        R.compare(proc, rep, rtol=0, atol=0)
         return
     R.compare(proc, rep)
 
