@@ -22,7 +22,12 @@ DONE = _Done()
 
 
 class Collective:
-    def __init__(self, group=None):
+    """force_exchange=True issues the collectives even at world size 1 (the
+    engines then take their multi-rank paths): lets a one-GPU box run the
+    RCCL reduce-scatter / all-gather pipeline with its async Work handles
+    (tests/test_gpu_rccl.py).  Default: world size 1 is a local no-op."""
+
+    def __init__(self, group=None, force_exchange=False):
         self.group = group
         if dist.is_available() and dist.is_initialized():
             self.world = dist.get_world_size(group)
@@ -30,6 +35,9 @@ class Collective:
             self.backend = str(dist.get_backend(group)).lower()
         else:
             self.world, self.rank, self.backend = 1, 0, "none"
+        if force_exchange and self.backend == "none":
+            raise RuntimeError("Collective(force_exchange=True) needs an initialised process group")
+        self.exchange = self.world > 1 or bool(force_exchange)
 
     @property
     def rccl(self):
@@ -40,21 +48,21 @@ class Collective:
     # wait() orders the CURRENT stream after the collective, the host does not
     # block); every other case runs synchronously and returns DONE.
     def all_reduce_(self, t, async_op=False):
-        if self.world > 1:
+        if self.exchange:
             w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op and self.rccl)
             if async_op:
                 return w if w is not None else DONE
         return DONE if async_op else t
 
     def broadcast_(self, t, src=0):
-        if self.world > 1:
+        if self.exchange:
             dist.broadcast(t, src=src, group=self.group)
         return t
 
     def reduce_scatter(self, shard_out, full, async_op=False):
         """shard_out = rank's shard of sum over ranks of `full` (full is scratch:
         the gloo fallback reduces it in place)."""
-        if self.world == 1:
+        if not self.exchange:
             if shard_out.data_ptr() != full.data_ptr():
                 shard_out.copy_(full[: shard_out.numel()])
             return DONE if async_op else shard_out
@@ -72,7 +80,7 @@ class Collective:
     def all_gather_into(self, full, shard, async_op=False):
         """full[r*per:(r+1)*per] = shard of rank r.  `shard` may be the rank's
         own slice of `full` (in place)."""
-        if self.world == 1:
+        if not self.exchange:
             if full.data_ptr() != shard.data_ptr():
                 full[: shard.numel()].copy_(shard)
             return DONE if async_op else full

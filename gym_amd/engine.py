@@ -122,20 +122,20 @@ class MeanReduce:
     def __init__(self, coll: Collective, K_local, n, device, dtype, shard=None, chunks=None):
         self.coll, self.K_local, self.n = coll, int(K_local), int(n)
         self.K_total = coll.world * self.K_local
-        W = coll.world
-        self.shard = (coll.rccl and W > 1) if shard is None else (shard and W > 1)
+        W, X = coll.world, coll.exchange
+        self.shard = (coll.rccl and X) if shard is None else (shard and X)
         if self.shard:
             esz = torch.empty((), dtype=dtype).element_size()
             self.plan = ShardPlan(self.n, W, coll.rank, esz, chunks)
             self.rs_out = torch.empty(self.plan.per, device=device, dtype=dtype)
-        self.sum = torch.empty(n, device=device, dtype=dtype) if (W > 1 and K_local > 1 and not self.shard) else None
+        self.sum = torch.empty(n, device=device, dtype=dtype) if (X and K_local > 1 and not self.shard) else None
 
     def _divide(self, rs_shard, m, own):
         ops.replica_mean(rs_shard, own, divisor=self.K_total)
 
     def __call__(self, reps):
         K, n = self.K_local, self.n
-        if self.coll.world == 1:
+        if not self.coll.exchange:
             if K > 1:
                 ops.replica_mean(reps, reps, n=n)
             return
@@ -163,8 +163,8 @@ class DiLoCoOuter:
         self.coll, self.K_local = coll, int(K_local)
         self.K_total = coll.world * self.K_local
         self.hp = dict(lr=lr, momentum=momentum, nesterov=nesterov, dampening=dampening, weight_decay=weight_decay)
-        W = coll.world
-        self.shard = (coll.rccl and W > 1) if shard is None else (shard and W > 1)
+        W, X = coll.world, coll.exchange
+        self.shard = (coll.rccl and X) if shard is None else (shard and X)
         self.n = int(n)
         if self.shard:
             esz = torch.empty((), dtype=dtype).element_size()
@@ -177,7 +177,7 @@ class DiLoCoOuter:
         self.mom = torch.zeros(self.per, device=device, dtype=torch.float32) if momentum != 0 else None
         self.first = True
         self.dtype = dtype
-        self.sum = torch.empty(n, device=device, dtype=dtype) if (W > 1 and not self.shard) else None
+        self.sum = torch.empty(n, device=device, dtype=dtype) if (X and not self.shard) else None
         self.rs_out = torch.empty(self.per, device=device, dtype=dtype) if self.shard else None
         self.launch_elems = []  # elements per ga_diloco_outer launch of the last step (bench roofline)
 
@@ -202,9 +202,8 @@ class DiLoCoOuter:
 
     def __call__(self, reps):
         n = self.n
-        W = self.coll.world
         self.launch_elems = []
-        if W == 1:  # one kernel: read every replica, update, write every replica
+        if not self.coll.exchange:  # one kernel: read every replica, update, write every replica
             self._outer(reps[:, :n], self.K_total, reps[:, :n])
         elif not self.shard:  # gloo: all-reduce the sum, replicated update
             ops.replica_mean(reps, self.sum, n=n, divisor=1.0)
@@ -266,7 +265,7 @@ class Sparta:
         else:
             self.check()
             cap_used = self.cap
-        if self.coll.world == 1:  # every node is a local replica: one fused pass, no exchange
+        if not self.coll.exchange:  # every node is a local replica: one fused pass, no exchange
             ops.sparta_average_local(reps, n, float(self.K_total), mask=mask, seed=seed, iteration=iteration,
                                      p=self.p, skip=skip)
             return
@@ -295,14 +294,14 @@ class DeMoCodec:
         M = self.plan.M
         self.payload = torch.zeros(self.K_local, 2 * M, dtype=torch.int32, device=device)
         self.gathered = (torch.zeros(self.K_total, 2 * M, dtype=torch.int32, device=device)
-                         if coll.world > 1 else self.payload)
+                         if coll.exchange else self.payload)
 
     def encode(self, P, G, D, lr, decay, weight_decay):
         wdf = _f32(1.0 - lr * weight_decay) if weight_decay != 0.0 else 1.0
         ops.demo_encode(self.plan, P, G, D, self.payload, _f32(lr), _f32(decay), wdf)
 
     def exchange(self, all_gather=None):
-        if self.coll.world == 1:
+        if not self.coll.exchange:
             return
         if all_gather is None:
             self.coll.all_gather_into(self.gathered.view(-1), self.payload.view(-1))

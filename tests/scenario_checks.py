@@ -132,6 +132,28 @@ def check_eval_avg(res, world, golden_dir):
                 np.testing.assert_allclose(res[r][f"avg_{i}"], want, rtol=1e-6, atol=1e-7 * scale)
 
 
+def check_mnist_diloco(res, world, golden_dir):
+    """Each outer step = oracle.diloco.outer_step over the nodes' parameters as
+    they entered it (master chained from the shared start, momentum from the
+    previous outer step); every node leaves it holding the new master."""
+    from oracle import diloco as odiloco
+    n = res[0]["pre_0"].size
+    master = res[0]["init"][:n].copy()
+    assert all(np.array_equal(res[r]["init"], res[0]["init"]) for r in range(world))
+    mom = None
+    outer = 0
+    for t in range(5):
+        if t % 2 == 0 and t > 0:  # the gate sees local_step = t before its increment (diloco.py:62)
+            pre = [res[r][f"pre_{outer}"] for r in range(world)]
+            assert not np.array_equal(pre[0], pre[1])  # the nodes trained on different data
+            master, mom, _ = odiloco.outer_step(master, mom, pre)
+            for r in range(world):
+                got = res[r][f"after_{t}"][:n]
+                np.testing.assert_allclose(got, master, rtol=1e-6, atol=1e-9)
+            outer += 1
+    assert outer == 2
+
+
 def check_fedavg(res, world, golden_dir, island_size=None):
     nt = 3
     before = [[res[r][f"before_{i}"] for i in range(nt)] for r in range(world)]
@@ -180,7 +202,7 @@ def check_demo(res, world, golden_dir):
     tally.done()
 
 
-def check_engine(res, world, golden_dir, K_local=3):
+def check_engine(res, world, golden_dir, K_local=3, **_):
     """Every node of every rank ends equal to the oracle over all K_total nodes
     (reordered fp32 sums: RCCL/gloo ring order, 1e-6 relative)."""
     import strategy_scenarios as S
@@ -199,6 +221,27 @@ def check_engine(res, world, golden_dir, K_local=3):
             np.testing.assert_allclose(res[r]["d2"][k], m2, rtol=1e-6, atol=2e-8)
             np.testing.assert_allclose(res[r]["m_shard"][k], avg, rtol=1e-6, atol=2e-8)
             np.testing.assert_allclose(res[r]["m_plain"][k], avg, rtol=1e-6, atol=2e-8)
+    if "sparta" in res[0]:  # forced-exchange run (world 1): exact orders, bit-exact
+        x3 = [S.engine_node(j, n, salt=3) for j in range(KT)]
+        want = osparta.sparse_average(x3, osparta.philox_mask(n, 77, 5, 0.05))
+        for k in range(KT):
+            assert np.array_equal(res[0]["sparta"][k], want[k])
+        import demo_checks
+        from gym_amd.arena import ArenaLayout
+        L = ArenaLayout([(128, 128), (768,)])
+        g = res[0]["demo_g"]
+        tally = demo_checks.SignTally()
+        for shape, off, m in zip(L.shapes, L.offsets, L.numels):
+            grads = [g[k, off:off + m].reshape(shape) for k in range(KT)]
+            zeros = [np.zeros(shape, np.float32)] * KT
+            want_p, _, want_s, _, g_hat, margins = odemo.demo_step(zeros[0], zeros, grads, 0.01, detail=True)
+            for k in range(KT):
+                tally.check(res[0]["demo_sign"][k, off:off + m].reshape(shape), want_s,
+                            demo_checks.firm(g_hat, margins, shape), what=f"demo {shape} node {k}")
+                ok = res[0]["demo_sign"][k, off:off + m].reshape(shape) == want_s
+                np.testing.assert_allclose(res[0]["demo_p"][k, off:off + m].reshape(shape)[ok], want_p[ok],
+                                           rtol=0, atol=1e-7)
+        tally.done()
 
 
 def check_simple_adamw(res, world, golden_dir, steps=3):
@@ -225,4 +268,4 @@ def check_simple_adamw(res, world, golden_dir, steps=3):
 
 CHECKS = {"simple_adamw": check_simple_adamw, "engine": check_engine, "simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
           "sparta_philox": check_sparta_philox, "sparta_sel": check_sparta_sel,
-          "eval_avg": check_eval_avg, "fedavg": check_fedavg, "demo": check_demo}
+          "eval_avg": check_eval_avg, "mnist_diloco": check_mnist_diloco, "fedavg": check_fedavg, "demo": check_demo}

@@ -208,6 +208,40 @@ def sc_eval_avg(rank, world, dev, golden_dir):
             **{f"after_{i}": _host(p) for i, p in enumerate(model.parameters())}}
 
 
+def sc_mnist_diloco(rank, world, dev, golden_dir, steps=5, H=2):
+    """configs[0]: the MNIST CNN under DiLoCoStrategy (H=2), real forward/backward on each node's synthetic MNIST-shaped
+    batch, default AdamW inner optimizer (outer steps at local_step 2 and 4,
+    diloco.py:62).  Records each node's parameters right
+    before each outer step and after it (the checker replays the outer step
+    in the oracle)."""
+    import tiny_models
+    from gym_amd.strategy import DiLoCoStrategy
+    torch.manual_seed(0)
+    model = tiny_models.MnistCNN().to(dev)  # identical start on every node (TrainNode broadcasts rank 0's)
+    s = DiLoCoStrategy(H=H)
+    s._init_node(model, rank, world)
+    assert sum(p.numel() for p in model.parameters()) == 1_868_234
+    rec = {}
+    eng = s.engine
+
+    class Tap:
+        def __call__(self, reps):
+            rec[f"pre_{len(rec)}"] = _host(reps[0])
+            return eng(reps)
+    s.engine = Tap()
+    ds = tiny_models.mnist_like(n=16 * steps, seed=100 + rank)
+    out = {"init": _host(s.arena.flat)}
+    for t in range(steps):
+        s.zero_grad()
+        x, y = ds.tensors
+        loss = model((x[16 * t:16 * (t + 1)].to(dev), y[16 * t:16 * (t + 1)].to(dev)))
+        loss.backward()
+        s.step()
+        out[f"after_{t}"] = _host(s.arena.flat)
+    out.update(rec)
+    return out
+
+
 def sc_fedavg(rank, world, dev, golden_dir, island_size=None):
     from gym_amd.strategy import FedAvgStrategy, OptimSpec
     shapes = [(66, 32), (128,), (3, 7)]
@@ -285,12 +319,16 @@ def engine_node(j, n, salt=0):
     return (g.standard_normal(n) * 0.02).astype(np.float32)
 
 
-def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4):
+def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4, force=False):
     """Batched replicas on every rank (K_local nodes per process) through the
-    sharded, chunk-pipelined exchange: DiLoCo outer steps and the mean reduce."""
+    sharded, chunk-pipelined exchange: DiLoCo outer steps and the mean reduce.
+    force=True issues the collectives even at world size 1 (Collective
+    force_exchange: the RCCL pipeline on a one-GPU box), and adds SPARTA
+    (select -> all-reduce -> scatter) and DeMo (encode -> all-gather -> decode)
+    through their multi-rank paths."""
     from gym_amd.comm import Collective
     from gym_amd.engine import DiLoCoOuter, MeanReduce
-    coll = Collective()
+    coll = Collective(force_exchange=force)
     n = world * 64 * 10
     nodes = range(rank * K_local, (rank + 1) * K_local)
     reps = torch.from_numpy(np.stack([engine_node(j, n) for j in nodes])).to(dev)
@@ -306,22 +344,47 @@ def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4):
         r2 = torch.from_numpy(np.stack([engine_node(j, n, salt=2) for j in nodes])).to(dev)
         MeanReduce(coll, K_local, n, dev, torch.float32, shard=shard, chunks=3)(r2)
         out[tag] = _host(r2)
+    if force:
+        from gym_amd.engine import DeMoCodec, Sparta
+        from gym_amd.arena import ArenaLayout
+        r3 = torch.from_numpy(np.stack([engine_node(j, n, salt=3) for j in nodes])).to(dev)
+        sp = Sparta(coll, K_local, n, dev, torch.float32, 0.05)
+        sp(r3, seed=77, iteration=5)
+        sp.check()
+        out["sparta"] = _host(r3)
+        L = ArenaLayout([(128, 128), (768,)])
+        P = torch.zeros(K_local, L.n, device=dev)
+        D = torch.zeros(K_local, L.n, device=dev)
+        G = torch.from_numpy(np.stack([engine_node(j, L.n, salt=4) for j in nodes])).to(dev)
+        for k in range(K_local):  # zero padding, as the arena keeps it
+            for o, m, o2 in zip(L.offsets, L.numels, L.offsets[1:] + [L.n]):
+                G[k, o + m:o2] = 0
+        out["demo_g"] = _host(G)
+        codec = DeMoCodec(coll, K_local, L, dev)
+        codec(P, G, D, 0.01)
+        out["demo_p"] = _host(P)
+        out["demo_sign"] = _host(G)
     return out
 
 
 SCENARIOS = {"simple_adamw": sc_simple_adamw, "engine": sc_engine, "simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
              "sparta_sel": sc_sparta_sel, "eval_avg": sc_eval_avg,
+             "mnist_diloco": sc_mnist_diloco,
              "fedavg": sc_fedavg, "demo": sc_demo}
 
 
-def _worker(rank, world, port, name, device, fake, out_dir, golden_dir, kwargs):
+def _worker(rank, world, port, name, device, fake, out_dir, golden_dir, kwargs, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     if fake:
         import fake_ops
         fake_ops.install()
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: one rank per GPU
+        torch.cuda.set_device(torch.device(device))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(device))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         dev = torch.device(device)
         res = SCENARIOS[name](rank, world, dev, golden_dir, **kwargs)
@@ -330,10 +393,11 @@ def _worker(rank, world, port, name, device, fake, out_dir, golden_dir, kwargs):
         dist.destroy_process_group()
 
 
-def run(name, world, device, fake, out_dir, golden_dir, **kwargs):
+def run(name, world, device, fake, out_dir, golden_dir, backend="gloo", **kwargs):
     import torch.multiprocessing as mp
     port = free_port()
-    mp.spawn(_worker, args=(world, port, name, device, fake, out_dir, golden_dir, kwargs), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, name, device, fake, out_dir, golden_dir, kwargs, backend), nprocs=world,
+             join=True)
     res = []
     for r in range(world):
         with np.load(os.path.join(out_dir, f"r{r}.npz")) as f:

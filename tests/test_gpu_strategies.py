@@ -23,6 +23,7 @@ CASES = [
     ("sparta_sel", 2, {"kind": "shuffled"}), ("sparta_sel", 2, {"kind": "partitioned"}),
     ("sparta_sel", 3, {"kind": "philox"}),
     ("eval_avg", 2, {}), ("eval_avg", 3, {}),
+    ("mnist_diloco", 2, {}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),
     ("demo", 2, {}),
 ]

@@ -1,0 +1,65 @@
+"""Process-group setup (LocalTrainer._build_connection, exogym/trainer.py:310-351):
+RCCL ("nccl") when every process has a GPU of its own, gloo when nodes share
+GPUs; device placement rank % len(devices); 127.0.0.1 rendezvous; CPU/MPS
+devices refused (no CPU path).  Host logic only: torch.distributed and the
+device calls are stubbed."""
+import pytest
+import torch
+
+from gym_amd import trainer as T
+
+
+def test_select_backend():
+    assert T.select_backend(8, list(range(8))) == "nccl"
+    assert T.select_backend(4, list(range(8))) == "nccl"
+    assert T.select_backend(2, [0]) == "gloo"
+    assert T.select_backend(16, list(range(8))) == "gloo"
+
+
+@pytest.fixture
+def stub(monkeypatch):
+    calls = {}
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: calls.setdefault("set_device", d))
+    monkeypatch.setattr(T.dist, "init_process_group",
+                        lambda backend, **kw: calls.update(backend=backend, **kw))
+    return calls
+
+
+def _trainer(rank, num_nodes, devices=None, device="cuda", world=None):
+    tr = T.LocalTrainer(torch.nn.Linear(2, 2), None, None, start_port=30000)
+    tr.rank, tr.num_nodes, tr.devices, tr.device = rank, num_nodes, devices, device
+    if world is not None:
+        tr.world_size = world
+    return tr
+
+
+def test_one_gpu_per_node_is_rccl(stub):
+    tr = _trainer(rank=5, num_nodes=8)
+    tr._build_connection()
+    assert stub["backend"] == "nccl" and stub["world_size"] == 8 and stub["rank"] == 5
+    assert stub["device_id"] == torch.device("cuda:5") and stub["set_device"] == 5
+    assert tr.device == torch.device("cuda:5")
+    import os
+    assert os.environ["MASTER_ADDR"] == "127.0.0.1" and os.environ["MASTER_PORT"] == "30000"
+
+
+def test_shared_gpus_are_gloo(stub):
+    tr = _trainer(rank=3, num_nodes=4, devices=[0, 1])
+    tr._build_connection()
+    assert stub["backend"] == "gloo" and "device_id" not in stub
+    assert stub["set_device"] == 1 and tr.device == torch.device("cuda:1")
+
+
+def test_replica_processes_use_rccl(stub):
+    """16 nodes on 8 GPUs: 8 processes hosting 2 nodes each, RCCL between them."""
+    tr = _trainer(rank=7, num_nodes=16, world=8)
+    tr._build_connection()
+    assert stub["backend"] == "nccl" and stub["world_size"] == 8 and stub["device_id"] == torch.device("cuda:7")
+
+
+@pytest.mark.parametrize("device", ["cpu", "mps"])
+def test_cpu_devices_are_refused(stub, device):
+    with pytest.raises(ValueError, match="Invalid device"):
+        _trainer(rank=0, num_nodes=2, device=device)._build_connection()

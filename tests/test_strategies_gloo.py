@@ -13,13 +13,14 @@ CASES = [
     ("simple", 2, {}), ("simple", 3, {}), ("simple", 3, {"shard": True, "chunks": 3}),
     ("diloco", 3, {}), ("diloco", 3, {"shard": True}), ("diloco", 3, {"shard": True, "chunks": 5}),
     ("simple_adamw", 2, {}), ("simple_adamw", 3, {}),
-    ("engine", 3, {}), ("engine", 2, {"chunks": 1}),
+    ("engine", 3, {}), ("engine", 2, {"chunks": 1}), ("engine", 1, {"force": True}),
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": False}),
     ("sparta_philox", 2, {}),
     ("sparta_sel", 2, {"kind": "random"}), ("sparta_sel", 3, {"kind": "random"}),
     ("sparta_sel", 2, {"kind": "shuffled"}), ("sparta_sel", 2, {"kind": "partitioned"}),
     ("sparta_sel", 3, {"kind": "philox"}),
     ("eval_avg", 2, {}), ("eval_avg", 3, {}),
+    ("mnist_diloco", 2, {}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),
     ("demo", 2, {}),
 ]
