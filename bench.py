@@ -12,9 +12,17 @@ value = node-parameter bytes averaged per second over the whole job
         = K_total * 4 * N_params / t_step  ("param GB/s"); ms_per_step = t_step.
 roofline = the fused ga_diloco_outer kernel: algorithmic HBM bytes per launch
         ((2*K_local + 4) * 4 * n: read every replica, master, momentum; write
-        them back) / its HIP-event-timed duration, against 8 TB/s.
-cpu_baseline = the numpy oracle's outer step (oracle/diloco.py) on rank 0, on a
-        bounded slice of the same arena, single thread.
+        them back) / its HIP-event-timed duration, against 8 TB/s.  "traffic"
+        = HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE x2 on
+        gfx950, WRITE_SIZE) of this same configuration, run by this script as
+        child processes before it touches the GPU itself; "copy_GBps" = a
+        float4 streaming copy (ga_stream_copy) timed in this process, what the
+        box streams.
+cpu_baseline = the reference's DiLoCo outer step restated per tensor in torch
+        (oracle/torch_diloco.py, bit-exact with the reference's golden run),
+        over gloo with 8 node processes x (cores/8) threads on this host, on
+        the full GPT-2 124M parameter list, N=1 only, run before the GPU is
+        initialised.
 
 Extra lines in "extras" (same timing rules, not the headline): SPARTA (32
 nodes in total, 32/G per GPU, p=0.005, Philox mask: configs[3]), SimpleReduce
@@ -131,29 +139,84 @@ class KernelTimer:
         return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else None
 
 
-def cpu_baseline_diloco(n_total, K, budget_s=12.0):
-    """Oracle outer step on a slice of the arena (rank 0, one host thread)."""
-    sys.path.insert(0, ROOT)
-    from oracle import diloco as odiloco
-    n = min(n_total, 8 * 1024 * 1024)
-    rng = np.random.default_rng(0)
-    master = (rng.standard_normal(n, dtype=np.float32) * 0.02).astype(np.float32)
-    reps = [(master + rng.standard_normal(n, dtype=np.float32) * 1e-3).astype(np.float32) for _ in range(K)]
-    mom = np.zeros(n, np.float32)
+def host_cores():
+    """CPU share of this process: the job's thread budget (OMP_NUM_THREADS is
+    set to the box's share on the GPU pool), capped by the visible CPUs."""
+    n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(env))) if env and env.isdigit() else n
+
+
+def cpu_baseline_diloco(model, K, steps=3, warmup=1):
+    """The reference's outer step (oracle/torch_diloco.py, per-tensor torch over
+    gloo: K node processes x cores//K threads) on the full parameter list."""
+    from oracle.torch_diloco import time_outer_step
+    shapes = MODELS[model]()
+    cores = host_cores()
+    t, threads = time_outer_step(shapes, nodes=K, cores=cores, steps=steps, warmup=warmup)
+    n = numel(shapes)
+    return {"value": round(K * 4 * n / t / 1e9, 4), "unit": "GB/s", "cores": K * threads, "kind": "port",
+            "ms_per_step": round(t * 1e3, 1), "nproc": os.cpu_count(), "threads_per_process": threads,
+            "sample": f"DiLoCo outer step (all-reduce+divide, rank-0 SGD-Nesterov on the master, broadcast) of "
+                      f"{model} ({n} params, {len(shapes)} tensors) over {K} gloo processes x {threads} threads "
+                      f"(oracle/torch_diloco.py, the reference's per-tensor torch ops, bit-exact with "
+                      f"tests/golden/diloco.npz), full size, {steps} timed steps after {warmup} warmup; "
+                      f"value = {K} x 4 x {n} B / step time"}
+
+
+def pmc_traffic_live(args, alg_bytes_expected=None, timeout=150):
+    """HBM bytes per ga_diloco_outer launch from two rocprofv3 PMC passes of
+    this configuration (FETCH_SIZE and WRITE_SIZE need passes of their own),
+    run as child processes.  MI355X_MICROARCH.md: counters in KiB; on gfx950
+    FETCH_SIZE reports half the bytes of wide coalesced reads (doubled here).
+    Returns (bytes, note)."""
+    import shutil
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import counter_values
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    vals = {}
+    env = {**os.environ, "TMPDIR": "/tmp"}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="ga_pmc_", dir="/tmp")
+        cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.join(ROOT, "bench.py"), "--pmc-child", "--model", args.model,
+               "--replicas", str(args.replicas)]
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE)
+        except subprocess.TimeoutExpired:
+            return None, f"rocprofv3 --pmc {counter} timed out"
+        v = counter_values(d, counter, "diloco_outer")
+        shutil.rmtree(d, ignore_errors=True)
+        if r.returncode != 0 or not v:
+            return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode}): {r.stderr.decode()[-200:]}"
+        vals[counter] = float(np.median(v))
+    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    return traffic, (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this configuration (median over the "
+                     f"launches; FETCH_SIZE x2 for gfx950 wide reads, KiB -> B): read "
+                     f"{2.0 * vals['FETCH_SIZE'] * 1024.0:.4g} B + write {vals['WRITE_SIZE'] * 1024.0:.4g} B")
+
+
+def stream_copy_rate(dev, nbytes=2 << 30, reps=10):
+    """GB/s (read + write bytes) of a float4 streaming copy in this process."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(1.0)
+    ops.stream_copy(src, dst)
     times = []
-    t_end = time.perf_counter() + budget_s
-    while time.perf_counter() < t_end or len(times) < 2:
-        t0 = time.perf_counter()
-        m2, b2, _ = odiloco.outer_step(master, mom, reps)
-        reps = [m2] * K  # write-back into every node, as the step does
-        times.append(time.perf_counter() - t0)
-        if len(times) >= 50:
-            break
-    t = float(np.median(times))
-    return {"value": round(K * 4 * n / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/diloco.outer_step, K={K} nodes x {n} fp32 elements (first {n} of the "
-                      f"{n_total}-element arena), median of {len(times)} steps, {t * 1e3:.1f} ms/step; "
-                      f"scaled per node-parameter byte"}
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.stream_copy(src, dst)
+        e1.record()
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1))
+    del src, dst
+    return 2 * nbytes / (float(np.median(times)) * 1e-3) / 1e9
 
 
 def bench_diloco(args, coll, dev):
@@ -183,20 +246,19 @@ def bench_diloco(args, coll, dev):
     else:  # gloo rehearsal: read the all-reduced sum, master, mom; write master, mom, every replica
         alg_bytes = (5 + K) * per * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "pmc_traffic_diloco.json")
-    if coll.world == 1 and os.path.exists(tfile):
-        # HBM bytes per launch from the committed rocprofv3 PMC passes of this
-        # same configuration (tools/pmc_traffic.py; FETCH_SIZE x2 on gfx950)
-        pmc = json.load(open(tfile))
-        if pmc.get("algorithmic_bytes_per_launch") == alg_bytes:
-            traffic = pmc["traffic_bytes_per_launch"]
+    traffic, tnote = getattr(args, "pmc", None) or (None, "not measured (N > 1 or --no-pmc)")
+    if coll.world > 1:
+        traffic, tnote = None, "not measured at N > 1"
+    copy = None if args.pmc_child else stream_copy_rate(dev)
     out = {
         "ms_per_step": t * 1e3, "value": value, "K_total": K_total, "n_params": n_params,
         "kernel_ms": kern_ms, "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "ga_diloco_outer", "bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4)},
+            "traffic_over_alg": round(traffic / alg_bytes, 6) if traffic else None, "traffic_source": tnote,
+            "kernel": "ga_diloco_outer", "bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),
+            "copy_GBps": round(copy, 1) if copy else None,
+            "frac_of_copy": round(achieved / copy, 4) if copy else None},
     }
     if coll.world > 1:
         S = 4 * n
@@ -347,7 +409,24 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--only", default=None, help="diloco|sparta|simple|demo|adamw (profiling runs)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    single = args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    if args.pmc_child:  # a rocprofv3 PMC pass: the headline kernel only, a few launches
+        coll = setup_dist(1)
+        dev = torch.device("cuda", 0)
+        bench_diloco(argparse.Namespace(**{**vars(args), "steps": 3, "warmup": 1}), coll, dev)
+        return
+    # host-side legs first, while this process has not touched the GPU (the
+    # children are started by fork+exec; none of them runs in a GPU-initialised process)
+    cpu = None
+    if single and not args.no_cpu_baseline and args.only is None:
+        cpu = cpu_baseline_diloco(args.model, args.replicas)
+    args.pmc = (None, "not measured (N > 1 or --no-pmc)")
+    if single and not args.no_pmc and args.only is None:
+        args.pmc = pmc_traffic_live(args)
 
     coll = setup_dist(args.gpus)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -384,9 +463,6 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    cpu = None
-    if not args.no_cpu_baseline and coll.world == 1:  # the CPU leg is timed at N=1 only
-        cpu = cpu_baseline_diloco(head["n_params"], args.replicas)
     K_total = head["K_total"]
     line = {
         "metric": "strategy-step param GB/s (%HBM/xGMI peak) + ms/outer step, GPT-2 124M, 1-8 GPUs",

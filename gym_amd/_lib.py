@@ -16,6 +16,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gym_amd.h")
 
 GA_F32 = 0
 GA_BF16 = 1
+GA_LAYOUT_ROWS = 0
+GA_LAYOUT_ELEM_MAJOR = 1
 
 c_i32, c_i64, c_u32, c_u64, c_f32, c_f64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_float, ctypes.c_double)
@@ -44,15 +46,16 @@ class DemoRowGroup(ctypes.Structure):
 SIGNATURES = {
     "ga_abi_version": (c_i32, []),
     "ga_last_error": (ctypes.c_char_p, []),
+    "ga_stream_copy": (c_i32, [c_p, c_p, c_i64, c_p]),
     "ga_replica_mean": (c_i32, [c_i32, c_p, c_i64, c_i64, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_p]),
     "ga_diloco_outer": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_i32, c_i32, c_f32, c_f32,
                                 c_f32, c_f32, c_i32, c_p, c_i64, c_i64, c_p]),
     "ga_sparta_workspace_bytes": (c_i64, [c_i64]),
     "ga_sparta_threshold": (c_u32, [c_f64]),
-    "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_p, c_u64, c_u64, c_u32, c_p, c_i64, c_i64,
+    "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_u32, c_p, c_i64, c_i64,
                                  c_p, c_p, c_p, c_p, c_p]),
-    "ga_sparta_scatter": (c_i32, [c_i32, c_p, c_p, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_p]),
-    "ga_sparta_average_local": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_p, c_u64, c_u64, c_u32, c_p, c_i64,
+    "ga_sparta_scatter": (c_i32, [c_i32, c_p, c_p, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_i32, c_p]),
+    "ga_sparta_average_local": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_u32, c_p, c_i64,
                                         c_f32, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "ga_demo_tensor_bytes": (c_i32, []),
     "ga_demo_encode": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32,

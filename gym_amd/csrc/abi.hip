@@ -27,6 +27,42 @@ int check_launch(const char* what) {
 
 }  // namespace ga
 
+namespace ga {
+
+// Streaming copy: each lane moves 4 float4 (loads issued back to back, then
+// the stores); a workgroup covers 1024 contiguous float4 (16 KiB).
+__global__ __launch_bounds__(256) void stream_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                          int64_t nvec) {
+    const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = base + u * 256;
+        if (i < nvec) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = base + u * 256;
+        if (i < nvec) dst[i] = v[u];
+    }
+}
+
+}  // namespace ga
+
+extern "C" GA_API int ga_stream_copy(const void* src, void* dst, int64_t nbytes, hipStream_t stream) {
+    ga::clear_error();
+    GA_REQUIRE(nbytes >= 0 && nbytes % 16 == 0, "ga_stream_copy: nbytes must be a multiple of 16");
+    GA_REQUIRE(((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % 16) == 0, "ga_stream_copy: 16-byte alignment");
+    if (nbytes == 0) return GA_OK;
+    GA_REQUIRE(src && dst, "ga_stream_copy: null buffer");
+    const int64_t nvec = nbytes / 16;
+    const int64_t grid = ga::ceil_div(nvec, 1024);
+    GA_REQUIRE(grid < (int64_t)INT32_MAX, "ga_stream_copy: too large");
+    hipLaunchKernelGGL(ga::stream_copy_kernel, dim3((unsigned)grid), dim3(256), 0, stream, (const float4*)src,
+                       (float4*)dst, nvec);
+    return ga::check_launch("ga_stream_copy");
+}
+
 extern "C" GA_API int ga_abi_version(void) { return 100; }
 
 extern "C" GA_API const char* ga_last_error(void) { return ga::g_err; }

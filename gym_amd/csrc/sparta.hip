@@ -184,7 +184,21 @@ __global__ __launch_bounds__(kScanBlock) void sparta_scan_kernel(const int32_t* 
 // load the (element, replica) pairs densely (one load per lane, no idle lanes
 // on sparse tiles) into LDS, and one lane per element sums its K values in
 // ascending replica order.
+//
+// Replica-set layouts (Rep): replica k of element i is at i*ei + k*ek.
+//   [K, ld] rows (ek = ld, ei = 1): consecutive lanes read consecutive selected
+//     elements of ONE replica (same 16 KB of a row -> few DRAM pages), but every
+//     (element, replica) is a separate random 4-B word;
+//   [n, ld] element-major (ei = ld >= K, ek = 1): consecutive lanes read the K
+//     replicas of ONE element, i.e. one element's K=32 fp32 values are one
+//     128-B line -- the gather/write-back moves whole lines.
 constexpr int kGatherSlots = 2048;  // floats of LDS for the (element, replica) values
+
+struct Rep {
+    int64_t ek, ei;  // strides of replica and element
+    bool em;         // element-major
+    __device__ __forceinline__ int64_t at(int64_t i, int64_t k) const { return i * ei + k * ek; }
+};
 
 // With divisor > 0 the kernel also finishes the step for a single process
 // (ga_sparta_average_local): each selected element's average is written back
@@ -192,7 +206,7 @@ constexpr int kGatherSlots = 2048;  // floats of LDS for the (element, replica) 
 // (full-line write-backs instead of partial writes from a later scatter pass).
 template <typename T>
 __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t n, const int32_t* tile_offsets,
-                                                                 T* src, int64_t K, int64_t ld,
+                                                                 T* src, int64_t K, Rep R,
                                                                  int64_t cap, int32_t* __restrict__ idx,
                                                                  T* __restrict__ vals, float divisor) {
     __shared__ int wave_tot[4];
@@ -217,12 +231,12 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
     __syncthreads();
     // entries per pass: as many as fit K values each in the LDS slots
     const int per_pass = K >= kGatherSlots ? 1 : (kGatherSlots / K < kSpBlock ? kGatherSlots / (int)K : kSpBlock);
+    const int Ki = (int)(K < kGatherSlots ? K : kGatherSlots);
     for (int c0 = 0; c0 < total; c0 += per_pass) {
         const int ce = (total - c0) < per_pass ? (total - c0) : per_pass;
         if (K <= kGatherSlots) {
-            // replica-major lanes: consecutive lanes read consecutive selected
-            // elements of ONE replica (same 16 KB tile -> few DRAM pages)
-            const int Ki = (int)K;
+            // lane f -> (element e, replica k): replica-major for [K, ld] rows,
+            // element-major for [n, ld] (one element's replicas on adjacent lanes)
             // every lane's loads of the pass issued back to back (one HBM latency
             // per pass instead of one per load), then staged into LDS
             constexpr int kLoads = kGatherSlots / kSpBlock;
@@ -231,15 +245,15 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
             for (int u = 0; u < kLoads; ++u) {
                 const int f = threadIdx.x + u * kSpBlock;
                 if (f < ce * Ki) {
-                    const int k = f / ce, e = f - k * ce;
-                    v[u] = Elem<T>::load(src + (int64_t)k * ld + tile0 + sel_list[c0 + e]);
+                    const int k = R.em ? f % Ki : f / ce, e = R.em ? f / Ki : f - k * ce;
+                    v[u] = Elem<T>::load(src + R.at(tile0 + sel_list[c0 + e], k));
                 }
             }
 #pragma unroll
             for (int u = 0; u < kLoads; ++u) {
                 const int f = threadIdx.x + u * kSpBlock;
                 if (f < ce * Ki) {
-                    const int k = f / ce, e = f - k * ce;
+                    const int k = R.em ? f % Ki : f / ce, e = R.em ? f / Ki : f - k * ce;
                     gv[e * Ki + k] = v[u];
                 }
             }
@@ -254,8 +268,8 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
             __syncthreads();
             if (divisor > 0.f) {
                 for (int f = threadIdx.x; f < ce * Ki; f += kSpBlock) {
-                    const int k = f / ce, e = f - k * ce;
-                    Elem<T>::store(src + (int64_t)k * ld + tile0 + sel_list[c0 + e], gavg[e]);
+                    const int k = R.em ? f % Ki : f / ce, e = R.em ? f / Ki : f - k * ce;
+                    Elem<T>::store(src + R.at(tile0 + sel_list[c0 + e], k), gavg[e]);
                 }
                 __syncthreads();
             }
@@ -263,28 +277,37 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
             const int64_t i = tile0 + sel_list[c0];
             float acc = 0.f;
             if (threadIdx.x == 0)
-                for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + k * ld + i);
+                for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + R.at(i, k));
             const int64_t pos = out0 + c0;
             if (threadIdx.x == 0 && vals && pos < cap) Elem<T>::store(vals + pos, acc);
             if (threadIdx.x == 0 && divisor > 0.f) {
                 const float a = acc / divisor;
-                for (int64_t k = 0; k < K; ++k) Elem<T>::store(src + k * ld + i, a);
+                for (int64_t k = 0; k < K; ++k) Elem<T>::store(src + R.at(i, k), a);
             }
         }
     }
 }
 
-// Scatter: one lane per (element, replica) pair, so every lane stores;
-// replicas on the grid's y dimension (no per-lane division).
+// Scatter: one lane per (element, replica) pair, so every lane stores.
+// [K, ld] rows: replicas on the grid's y dimension (no per-lane division);
+// element-major: consecutive lanes store the K replicas of one element (one
+// line per element at K = 32 fp32).
 template <typename T>
 __global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __restrict__ vals,
                                                                   const int32_t* __restrict__ idx,
                                                                   const int64_t* __restrict__ count, int64_t cap,
-                                                                  float divisor, T* dst, int64_t K, int64_t ld) {
+                                                                  float divisor, T* dst, int64_t K, Rep R) {
     const int64_t m = count[0] < cap ? count[0] : cap;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (R.em) {
+        for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m * K; t += stride) {
+            const int64_t j = t / K, k = t - j * K;
+            Elem<T>::store(dst + R.at(idx[j], k), Elem<T>::load(vals + j) / divisor);
+        }
+        return;
+    }
     for (int64_t k = blockIdx.y; k < K; k += gridDim.y) {
-        T* d = dst + k * ld;
+        T* d = dst + k * R.ek;
         for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride)
             Elem<T>::store(d + idx[j], Elem<T>::load(vals + j) / divisor);
     }
@@ -292,8 +315,16 @@ __global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __res
 
 static int64_t sparta_tiles(int64_t n) { return ceil_div(n, kSpTile); }
 
+static Rep make_rep(int64_t ld, int layout) {
+    Rep R;
+    R.em = layout == GA_LAYOUT_ELEM_MAJOR;
+    R.ek = R.em ? 1 : ld;
+    R.ei = R.em ? ld : 1;
+    return R;
+}
+
 template <typename T>
-static int launch_select(const void* src, int64_t K, int64_t ld, int64_t n, const Pred& P, int64_t cap,
+static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pred& P, int64_t cap,
                          int32_t* idx, void* vals, int64_t* count, void* work, float divisor, hipStream_t stream) {
     const int64_t ntiles = sparta_tiles(n);
     int32_t* tile_offsets = nullptr;
@@ -308,7 +339,7 @@ static int launch_select(const void* src, int64_t K, int64_t ld, int64_t n, cons
         if (int e = check_launch("ga_sparta_select(scan)")) return e;
     }
     hipLaunchKernelGGL((sparta_select_kernel<T>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
-                       tile_offsets, (T*)src, K, ld, cap, idx, (T*)vals, divisor);
+                       tile_offsets, (T*)src, K, R, cap, idx, (T*)vals, divisor);
     return check_launch("ga_sparta_select(gather)");
 }
 
@@ -329,7 +360,7 @@ extern "C" GA_API uint32_t ga_sparta_threshold(double p) {
     return u;
 }
 
-extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld, int64_t n,
+extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld, int layout, int64_t n,
                                        const uint8_t* mask, uint64_t seed, uint64_t iteration,
                                        uint32_t threshold, const int64_t* skip, int64_t nskip,
                                        int64_t cap, int32_t* idx, void* vals,
@@ -338,7 +369,8 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "ga_sparta_select: n=%lld out of int32 index range", (long long)n);
     GA_REQUIRE(K >= 1 && cap >= 0, "ga_sparta_select: bad K=%lld cap=%lld", (long long)K, (long long)cap);
     GA_REQUIRE(count && work, "ga_sparta_select: null count/work");
-    GA_REQUIRE(K == 1 || ld >= n, "ga_sparta_select: ld < n");
+    GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_select: bad layout %d", layout);
+    GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_select: ld too small");
     GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_select: threshold > 2^24");
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_select: mask must be 16-byte aligned");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_select: bad skip table");
@@ -353,14 +385,16 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     P.skip = skip;
     P.nskip = (int32_t)nskip;
     switch (dtype) {
-        case GA_F32: return launch_select<float>(src, K, ld, n, P, cap, idx, vals, count, work, 0.f, stream);
+        case GA_F32:
+            return launch_select<float>(src, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work, 0.f, stream);
         case GA_BF16:
-            return launch_select<__hip_bfloat16>(src, K, ld, n, P, cap, idx, vals, count, work, 0.f, stream);
+            return launch_select<__hip_bfloat16>(src, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work, 0.f,
+                                                 stream);
         default: set_error("ga_sparta_select: unknown dtype %d", dtype); return GA_EINVAL;
     }
 }
 
-extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
+extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int layout, int64_t n,
                                               const uint8_t* mask, uint64_t seed, uint64_t iteration,
                                               uint32_t threshold, const int64_t* skip, int64_t nskip,
                                               float divisor, int32_t* idx, void* vals,
@@ -369,7 +403,8 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
     GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "ga_sparta_average_local: n=%lld out of range", (long long)n);
     GA_REQUIRE(K >= 1 && cap >= 0, "ga_sparta_average_local: bad K/cap");
     GA_REQUIRE(divisor > 0.0f, "ga_sparta_average_local: divisor must be > 0");
-    GA_REQUIRE(K == 1 || ld >= n, "ga_sparta_average_local: ld < n");
+    GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_average_local: bad layout");
+    GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_average_local: ld too small");
     GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_average_local: threshold > 2^24");
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_average_local: mask alignment");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_average_local: bad skip table");
@@ -386,31 +421,38 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
     P.skip = skip;
     P.nskip = (int32_t)nskip;
     switch (dtype) {
-        case GA_F32: return launch_select<float>(reps, K, ld, n, P, cap, idx, vals, count, work, divisor, stream);
+        case GA_F32:
+            return launch_select<float>(reps, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work, divisor,
+                                        stream);
         case GA_BF16:
-            return launch_select<__hip_bfloat16>(reps, K, ld, n, P, cap, idx, vals, count, work, divisor, stream);
+            return launch_select<__hip_bfloat16>(reps, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work,
+                                                 divisor, stream);
         default: set_error("ga_sparta_average_local: unknown dtype %d", dtype); return GA_EINVAL;
     }
 }
 
 extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx, const int64_t* count,
-                                        int64_t cap, float divisor, void* dst, int64_t K, int64_t ld,
+                                        int64_t cap, float divisor, void* dst, int64_t K, int64_t ld, int layout,
                                         hipStream_t stream) {
     clear_error();
     GA_REQUIRE(K >= 1 && cap >= 0, "ga_sparta_scatter: bad K/cap");
+    GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_scatter: bad layout");
+    GA_REQUIRE(layout == GA_LAYOUT_ROWS || ld >= K, "ga_sparta_scatter: element stride < K");
     if (cap == 0) return GA_OK;
     GA_REQUIRE(vals && idx && count && dst, "ga_sparta_scatter: null buffer");
     GA_REQUIRE(divisor != 0.0f, "ga_sparta_scatter: divisor is 0");
     const int gx = stream_grid(cap, kSpBlock);
-    const dim3 grid(gx > 64 ? 64 : gx, (unsigned)(K < 65535 ? K : 65535));
+    const Rep R = make_rep(ld, layout);
+    const dim3 grid = R.em ? dim3((unsigned)stream_grid(cap * K, kSpBlock)) :
+                             dim3(gx > 64 ? 64 : gx, (unsigned)(K < 65535 ? K : 65535));
     switch (dtype) {
         case GA_F32:
             hipLaunchKernelGGL((sparta_scatter_kernel<float>), grid, dim3(kSpBlock), 0, stream,
-                               (const float*)vals, idx, count, cap, divisor, (float*)dst, K, ld);
+                               (const float*)vals, idx, count, cap, divisor, (float*)dst, K, R);
             break;
         case GA_BF16:
             hipLaunchKernelGGL((sparta_scatter_kernel<__hip_bfloat16>), grid, dim3(kSpBlock), 0, stream,
-                               (const __hip_bfloat16*)vals, idx, count, cap, divisor, (__hip_bfloat16*)dst, K, ld);
+                               (const __hip_bfloat16*)vals, idx, count, cap, divisor, (__hip_bfloat16*)dst, K, R);
             break;
         default: set_error("ga_sparta_scatter: unknown dtype %d", dtype); return GA_EINVAL;
     }

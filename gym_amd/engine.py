@@ -223,10 +223,14 @@ def sparta_capacity(n, p):
 
 class Sparta:
     """SPARTA sparse averaging over the whole arena in one select/gather, one
-    all-reduce of the packed values, one scatter."""
+    all-reduce of the packed values, one scatter.  layout="rows": the replica
+    set is [K_local, ld] (the training loop's layout); "elem": [n, K_local]
+    element-major, where one element's K replicas share a line (batched-replica
+    sets built for the step alone, e.g. the bench's configs[3])."""
 
-    def __init__(self, coll: Collective, K_local, n, device, dtype, p):
+    def __init__(self, coll: Collective, K_local, n, device, dtype, p, layout="rows"):
         self.coll, self.K_local, self.n, self.p = coll, int(K_local), int(n), float(p)
+        self.layout = layout
         self.K_total = coll.world * self.K_local
         self.device, self.dtype = torch.device(device), dtype
         self.cap = sparta_capacity(n, self.p)
@@ -267,12 +271,12 @@ class Sparta:
             cap_used = self.cap
         if not self.coll.exchange:  # every node is a local replica: one fused pass, no exchange
             ops.sparta_average_local(reps, n, float(self.K_total), mask=mask, seed=seed, iteration=iteration,
-                                     p=self.p, skip=skip)
+                                     p=self.p, skip=skip, layout=self.layout)
             return
         ops.sparta_select(reps, n, cap_used, self.idx, self.vals, self.count, self.work, mask=mask, seed=seed,
-                          iteration=iteration, p=self.p, skip=skip)
+                          iteration=iteration, p=self.p, skip=skip, layout=self.layout)
         self.coll.all_reduce_(self.vals[:cap_used])
-        ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps)
+        ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps, layout=self.layout)
         if mask is None:  # overflow flag read back asynchronously, checked next step
             self._flag_host.copy_(self.count, non_blocking=True)
             if self.device.type == "cuda":

@@ -5,7 +5,9 @@ dtypes on the host (so a kernel never runs on operands it was not sized for),
 and enqueues the kernel on torch's current stream.  There is no CPU path:
 a CPU tensor raises.
 
-Replica sets are 2-D tensors [K, ld]; a 1-D tensor is one replica.
+Replica sets are 2-D tensors [K, ld]; a 1-D tensor is one replica.  The
+SPARTA wrappers also take element-major replica sets (layout="elem"): a 2-D
+tensor [n, K] whose row i holds element i of every replica.
 """
 import ctypes
 import os
@@ -104,6 +106,24 @@ def sparta_workspace(n, device):
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
+def _sparta_set(t, layout):
+    """(K, ld, layout code) of a SPARTA replica set."""
+    t2 = _as2d(t)
+    if layout == "rows":
+        K, ld = _rows_ld(t2)
+        return t2, K, ld, _lib.GA_LAYOUT_ROWS
+    if layout == "elem":
+        if t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError("element-major replica set must be a [n, K] tensor with unit replica stride")
+        return t, t.shape[1], t.stride(0), _lib.GA_LAYOUT_ELEM_MAJOR
+    raise ValueError(f"layout must be 'rows' or 'elem', got {layout!r}")
+
+
+def _rows_of(t2, code):
+    """Elements per replica available in a set."""
+    return t2.shape[0] if code == _lib.GA_LAYOUT_ELEM_MAJOR else t2.shape[1]
+
+
 def _skip_table(skip):
     """skip: None or an int64 device tensor [R, 2] of sorted disjoint [lo, hi)
     element ranges the Philox draw never selects."""
@@ -114,14 +134,16 @@ def _skip_table(skip):
     return skip, skip.shape[0]
 
 
-def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0, skip=None):
+def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0, skip=None,
+                  layout="rows"):
     """Compact the selected elements of [0, n) (mask != 0, or the Philox draw
     outside the `skip` ranges) into idx (int32) and vals (= sum over the
     replicas of src); count[0] = number selected, count[1] = overflow flag."""
-    src2 = _as2d(src)
-    _gpu(src2, idx, vals, count, work, mask, skip)
+    _gpu(src, idx, vals, count, work, mask, skip)
+    src2, K, ld, code = _sparta_set(src, layout)
+    if _rows_of(src2, code) < n:
+        raise ValueError("sparta_select: replica set shorter than n")
     skip, nskip = _skip_table(skip)
-    K, ld = _rows_ld(src2)
     if idx.dtype != torch.int32 or count.dtype != torch.int64 or count.numel() < 2:
         raise TypeError("sparta_select: idx int32, count int64[2]")
     if vals.dtype != src2.dtype or idx.numel() < cap or vals.numel() < cap:
@@ -132,21 +154,22 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
         if mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n:
             raise ValueError("sparta_select: mask must be uint8/bool with >= n elements")
     thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
-    check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, int(n), _p(mask), int(seed) & (2**64 - 1),
+    check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, code, int(n), _p(mask), int(seed) & (2**64 - 1),
                                  int(iteration) & (2**64 - 1), thr, _p(skip), nskip, int(cap), _p(idx), _p(vals),
                                  _p(count),
                                  _p(work), _stream()), "ga_sparta_select")
 
 
 def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0, idx=None, vals=None, cap=0,
-                         count=None, work=None, skip=None):
-    """Single-process SPARTA step over [K, ld] replicas: selected elements of
-    every replica <- (sum over replicas) / divisor, one pass (optional packed
-    idx/vals/count outputs as sparta_select)."""
-    r2 = _as2d(reps)
-    _gpu(r2, mask, idx, vals, count, work, skip)
+                         count=None, work=None, skip=None, layout="rows"):
+    """Single-process SPARTA step over a replica set ([K, ld] rows, or [n, K]
+    element-major): selected elements of every replica <- (sum over replicas)
+    / divisor, one pass (optional packed idx/vals/count outputs as sparta_select)."""
+    _gpu(reps, mask, idx, vals, count, work, skip)
+    r2, K, ld, code = _sparta_set(reps, layout)
+    if _rows_of(r2, code) < n:
+        raise ValueError("sparta_average_local: replica set shorter than n")
     skip, nskip = _skip_table(skip)
-    K, ld = _rows_ld(r2)
     if mask is not None and (mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n):
         raise ValueError("sparta_average_local: mask must be uint8/bool with >= n elements")
     if idx is not None:
@@ -155,20 +178,20 @@ def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0
         if idx.numel() < cap or vals.numel() < cap or work.numel() < lib().ga_sparta_workspace_bytes(int(n)):
             raise ValueError("sparta_average_local: output buffers too small")
     thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
-    check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, int(n), _p(mask), int(seed) & (2**64 - 1),
+    check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, code, int(n), _p(mask),
+                                        int(seed) & (2**64 - 1),
                                         int(iteration) & (2**64 - 1), thr, _p(skip), nskip, float(divisor),
                                         _p(idx), _p(vals),
                                         int(cap), _p(count), _p(work), _stream()), "ga_sparta_average_local")
 
 
-def sparta_scatter(vals, idx, count, cap, divisor, dst):
-    dst2 = _as2d(dst)
-    _gpu(vals, idx, count, dst2)
-    K, ld = _rows_ld(dst2)
+def sparta_scatter(vals, idx, count, cap, divisor, dst, layout="rows"):
+    _gpu(vals, idx, count, dst)
+    dst2, K, ld, code = _sparta_set(dst, layout)
     if vals.dtype != dst2.dtype:
         raise TypeError("sparta_scatter: dtype mismatch")
     check(lib().ga_sparta_scatter(_dtype_code(dst2), _p(vals), _p(idx), _p(count), int(cap), float(divisor),
-                                  _p(dst2), K, ld, _stream()), "ga_sparta_scatter")
+                                  _p(dst2), K, ld, code, _stream()), "ga_sparta_scatter")
 
 
 def demo_encode(plan, param, grad, delta, payload, lr, decay, wd_factor):
@@ -225,6 +248,15 @@ def demo_decode(plan, gathered, param, grad, lr):
     check(lib().ga_demo_decode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.B), _p(ga),
                                ga.stride(0), plan.M, S, _p(p2), _p(g2), K, ld, float(lr), _stream()),
           "ga_demo_decode")
+
+
+def stream_copy(src, dst):
+    """dst <- src as a float4 streaming copy (calibration helper)."""
+    _gpu(src, dst)
+    nb = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < nb or not src.is_contiguous() or not dst.is_contiguous():
+        raise ValueError("stream_copy: contiguous buffers, dst at least as large as src")
+    check(lib().ga_stream_copy(_p(src), _p(dst), nb, _stream()), "ga_stream_copy")
 
 
 def sumsq_partials(device, K=1):

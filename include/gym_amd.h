@@ -42,6 +42,13 @@ extern "C" {
 #define GA_F32 0
 #define GA_BF16 1
 
+/* replica-set layouts (SPARTA entry points):
+ *   GA_LAYOUT_ROWS        [K, ld]: replica k of element i at k*ld + i (every other kernel's layout)
+ *   GA_LAYOUT_ELEM_MAJOR  [n, ld]: replica k of element i at i*ld + k (ld >= K): the K replicas of
+ *                         one element are adjacent, so a sparse gather moves whole lines */
+#define GA_LAYOUT_ROWS 0
+#define GA_LAYOUT_ELEM_MAJOR 1
+
 /* ---- library ---------------------------------------------------------- */
 
 /* ABI version (major*100 + minor). */
@@ -49,6 +56,14 @@ GA_API int ga_abi_version(void);
 
 /* Message describing the last failure on the calling thread ("" if none). */
 GA_API const char* ga_last_error(void);
+
+/*
+ * Calibration helper (no reference counterpart): dst <- src, nbytes (a multiple
+ * of 16, 16-byte aligned buffers) as a float4 streaming copy.  bench.py times
+ * it in the same process as the step kernels, so a roofline fraction can be
+ * read against what the box actually streams.
+ */
+GA_API int ga_stream_copy(const void* src, void* dst, int64_t nbytes, hipStream_t stream);
 
 /* ---- mean reduce: SimpleReduce / FedAvg / DiLoCo averaging ------------- */
 
@@ -101,7 +116,8 @@ GA_API uint32_t ga_sparta_threshold(double p);
 
 /*
  * Select the SPARTA index set over an arena of n elements and gather the
- * selected values summed over the K local replicas.
+ * selected values summed over the K local replicas (replica set in `layout`,
+ * GA_LAYOUT_*).
  *   mask source: if mask != null, element i is selected iff mask[i] != 0
  *   (uint8 mask arena: rank 0's per-tensor index_selector masks, broadcast --
  *   sparta.py:32-37); otherwise the in-kernel Philox4x32-10 stream decides:
@@ -119,20 +135,21 @@ GA_API uint32_t ga_sparta_threshold(double p);
  * broadcast and gather of SparseCommunicator.communicate (sparta.py:24-38).
  */
 GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld,
-                            int64_t n, const uint8_t* mask, uint64_t seed,
+                            int layout, int64_t n, const uint8_t* mask, uint64_t seed,
                             uint64_t iteration, uint32_t threshold,
                             const int64_t* skip, int64_t nskip, int64_t cap,
                             int32_t* idx, void* vals, int64_t* count, void* work,
                             hipStream_t stream);
 
 /*
- * dst_k[idx[j]] = vals[j] / divisor for j < min(count[0], cap), k < K.
+ * dst_k[idx[j]] = vals[j] / divisor for j < min(count[0], cap), k < K
+ * (replica set in `layout`, GA_LAYOUT_*).
  * Replaces: `sparse_data /= num_nodes; param.masked_scatter_(mask, sparse_data)`
  * (sparta.py:40-42).
  */
 GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
                              const int64_t* count, int64_t cap, float divisor,
-                             void* dst, int64_t K, int64_t ld, hipStream_t stream);
+                             void* dst, int64_t K, int64_t ld, int layout, hipStream_t stream);
 
 /*
  * Single-process SPARTA step (every node is a local replica, no exchange):
@@ -142,7 +159,7 @@ GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
  * (no packed list, no count/scan pass); if given they are filled as by
  * ga_sparta_select.  Replaces sparta.py:24-44 for batched replicas.
  */
-GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
+GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int layout, int64_t n,
                                    const uint8_t* mask, uint64_t seed, uint64_t iteration,
                                    uint32_t threshold, const int64_t* skip, int64_t nskip,
                                    float divisor, int32_t* idx, void* vals,

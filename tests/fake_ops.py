@@ -60,7 +60,13 @@ def _skip_list(skip):
     return None if skip is None else [tuple(r) for r in skip.cpu().tolist()]
 
 
-def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0, skip=None):
+def _rows_view(t, layout):
+    return t.t() if layout == "elem" else _2d(t)
+
+
+def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0, skip=None,
+                  layout="rows"):
+    src = _rows_view(src, layout)
     m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
                                                                            skip=_skip_list(skip))
     sel = np.flatnonzero(m)
@@ -71,7 +77,8 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
     vals[: len(sel)] = torch.from_numpy(oreduce.mean_reduce(list(_np(_2d(src))[:, sel]), divisor=1)).to(vals.dtype)
 
 
-def sparta_scatter(vals, idx, count, cap, divisor, dst):
+def sparta_scatter(vals, idx, count, cap, divisor, dst, layout="rows"):
+    dst = _rows_view(dst, layout)
     m = min(int(count[0]), int(cap))
     ii = idx[:m].long()
     v = (vals[:m].float() / np.float32(divisor)).to(dst.dtype)
@@ -81,7 +88,8 @@ def sparta_scatter(vals, idx, count, cap, divisor, dst):
 
 
 def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0, idx=None, vals=None, cap=0,
-                         count=None, work=None, skip=None):
+                         count=None, work=None, skip=None, layout="rows"):
+    reps = _rows_view(reps, layout)
     m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
                                                                            skip=_skip_list(skip))
     r2 = _2d(reps)

@@ -274,6 +274,67 @@ def test_sparta_philox_skip_ranges(fused):
         assert np.array_equal(got[k], want[k])
 
 
+@pytest.mark.parametrize("K,use_mask,with_list", [(32, False, False), (32, False, True), (5, True, False),
+                                                   (64, False, False), (3000, False, False)])
+def test_sparta_average_local_element_major(K, use_mask, with_list):
+    """[n, K] element-major replica sets (one element's K replicas adjacent):
+    the same selection and ascending-replica fp32 mean as the [K, n] layout."""
+    from gym_amd import ops
+    n, p = (300_001, 0.01) if K < 1000 else (20_000, 0.002)
+    rng = np.random.default_rng(K + 7)
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    seed, it = 1234, 9
+    if use_mask:
+        m = rng.random(n) < 0.02
+        mask_t = torch.zeros(n + 15, dtype=torch.uint8, device=DEV)
+        mask_t[:n] = torch.from_numpy(m.astype(np.uint8)).to(DEV)
+    else:
+        m = osparta.philox_mask(n, seed, it, p)
+        mask_t = None
+    em = t(np.ascontiguousarray(x.T))  # [n, K]
+    kw = {}
+    if with_list:
+        cap = int(m.sum()) + 16
+        idx, count, work = _sparta_buffers(n, cap)
+        kw = dict(idx=idx, vals=torch.empty(cap, device=DEV), cap=cap, count=count, work=work)
+    ops.sparta_average_local(em, n, float(K), mask=mask_t, seed=seed, iteration=it, p=p, layout="elem", **kw)
+    want = osparta.sparse_average(list(x), m)
+    got = host(em).T
+    for k in range(K):
+        assert np.array_equal(got[k], want[k])
+    if with_list:
+        c = int(kw["count"][0].item())
+        assert c == int(m.sum()) and np.array_equal(kw["idx"][:c].cpu().numpy(), np.flatnonzero(m))
+
+
+def test_sparta_select_scatter_element_major_padded_rows():
+    """Element-major set with a row stride > K ([n, 40] buffer, K = 32 used):
+    select+gather, scatter; the 8 spare columns are never touched."""
+    from gym_amd import ops
+    n, p, K = 100_003, 0.02, 32
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    buf = torch.full((n, 40), 5.0, device=DEV)
+    buf[:, :K] = t(np.ascontiguousarray(x.T))
+    em = buf[:, :K]
+    seed, it = 77, 2
+    skip = [(100, 5000), (60_001, 60_017)]
+    m = osparta.philox_mask(n, seed, it, p, skip=skip)
+    cap = int(m.sum()) + 32
+    idx, count, work = _sparta_buffers(n, cap)
+    vals = torch.empty(cap, device=DEV)
+    sk = torch.tensor(skip, dtype=torch.int64, device=DEV)
+    ops.sparta_select(em, n, cap, idx, vals, count, work, seed=seed, iteration=it, p=p, skip=sk, layout="elem")
+    c = int(count[0].item())
+    assert c == int(m.sum()) and np.array_equal(idx[:c].cpu().numpy(), np.flatnonzero(m))
+    assert np.array_equal(host(vals)[:c], oreduce.mean_reduce(list(x[:, m]), divisor=1))
+    ops.sparta_scatter(vals, idx, count, cap, float(K), em, layout="elem")
+    want = osparta.sparse_average(list(x), m)
+    got = host(buf)
+    assert np.array_equal(got[:, :K].T, np.stack(want))
+    assert (got[:, K:] == 5.0).all()
+
+
 def test_sparta_overflow_flag():
     from gym_amd import ops
     n = 10_000
@@ -401,7 +462,9 @@ def test_demo_encode_decode_matches_oracle(K, wave):
         np.testing.assert_allclose(gP[0, off:off + nel].reshape(shape)[ok], want_p[ok], rtol=0, atol=1e-6)
         for k in range(1, K):
             assert np.array_equal(gP[k, off:off + nel], gP[0, off:off + nel])
-    tally.done()
+    # a near-tied chunk is excluded whole (64x64 = 25% of a 128x128 tensor), so on
+    # these few-chunk tensors the floor is lower than at full size (test_gpu_fullsize)
+    tally.done(min_firm=0.9)
     # padding between tensors stays exactly zero in every arena
     for arr in (gP, gD, gS):
         for o, nel, o2 in zip(L.offsets, L.numels, L.offsets[1:] + [L.n]):
