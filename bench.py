@@ -201,6 +201,13 @@ def pmc_traffic_live(args, alg_bytes_expected=None, timeout=150):
                      f"{2.0 * vals['FETCH_SIZE'] * 1024.0:.4g} B + write {vals['WRITE_SIZE'] * 1024.0:.4g} B")
 
 
+def under_profiler():
+    """True inside a rocprofv3 run (its tool library is preloaded and has
+    initialised the GPU): a nested rocprofv3 would have to exec from there."""
+    pre = os.environ.get("LD_PRELOAD", "") + os.environ.get("HSA_TOOLS_LIB", "")
+    return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def stream_copy_rate(dev, nbytes=2 << 30, reps=10):
     """GB/s (read + write bytes) of a float4 streaming copy in this process."""
     src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
@@ -270,35 +277,67 @@ def bench_diloco(args, coll, dev):
     return out
 
 
-def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m"):
+def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout_kind="elem"):
     """configs[3]: K=32 simulated nodes on one GPU, or the same 32 nodes sharded
-    32/G per GPU over G GPUs (strong: the node count is the config's)."""
+    32/G per GPU over G GPUs (strong: the node count is the config's).
+    layout_kind "elem": the replica set element-major [n, K] (one element's K
+    replicas adjacent: at K=32 fp32 one 128-B line per selected element);
+    "rows": [K, n], the replica training loop's layout (every selected
+    (element, replica) a separate random 4-B word)."""
     K = max(1, K_total // coll.world)
     shapes = MODELS[model]()
     layout = ArenaLayout(shapes)
     rs = synth_replicas(layout, K, coll.rank, dev)
-    eng = Sparta(coll, K, layout.n, dev, torch.float32, p)
+    reps = rs.data
+    conv_ms = None
+    if layout_kind == "elem":
+        # what moving the training loop's [K, n] set into the step's layout costs (untimed in the step)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        reps = rs.data.t().contiguous()  # [n, K]
+        e1.record()
+        e1.synchronize()
+        conv_ms = e0.elapsed_time(e1)
+        del rs
+        torch.cuda.empty_cache()
+    eng = Sparta(coll, K, layout.n, dev, torch.float32, p, layout=layout_kind)
+    timer = KernelTimer()
+    avg_local = ops.sparta_average_local
+    ops.sparta_average_local = timer.wrap(avg_local)
     it = [0]
 
     def step():
-        eng(rs.data, seed=42, iteration=it[0])
+        eng(reps, seed=42, iteration=it[0])
         it[0] += 1
 
-    t = timed_loop(step, args.steps, args.warmup, coll)
+    timer.on = True
+    try:
+        t = timed_loop(step, args.steps, args.warmup, coll)
+    finally:
+        ops.sparta_average_local = avg_local
+    kern = timer.mean_ms()
     eng.check()
     # the number selected (untimed; the fused single-GPU pass produces no list)
-    ops.sparta_select(rs.data, layout.n, eng.cap, eng.idx, eng.vals, eng.count, eng.work, seed=42, iteration=0, p=p)
+    ops.sparta_select(reps, layout.n, eng.cap, eng.idx, eng.vals, eng.count, eng.work, seed=42, iteration=0, p=p,
+                      layout=layout_kind)
     M = int(eng.count[0].item())
     alg = 2 * 4 * K * M + (8 * M if coll.world > 1 else 0)  # K-replica gather + write-back (+ idx/vals list)
-    # what HBM must move at its access granularity: each selected (element, replica)
-    # is a random 4-B word -> one 64-B read sector + one 32-B write sector
-    # (rocprofv3 FETCH_SIZE/WRITE_SIZE of this kernel: 1.18 GB + 0.61 GB per step)
-    sect = (64 + 32) * K * M
-    return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
-            "K_local": K, "K_total": K * coll.world, "p": p, "selected": M, "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1),
-            "sector_bytes": sect, "sector_GBps": round(sect / t / 1e9, 1),
-            "path": "fused select+gather+average+write-back" if coll.world == 1 else
-                    f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter"}
+    # what HBM must move at its access granularity: rows -> each selected (element,
+    # replica) is a random 4-B word = one 64-B read sector + one 32-B write sector;
+    # elem -> one element's K values are ceil(4K/64) whole 64-B sectors each way
+    sect = (64 + 32) * K * M if layout_kind == "rows" else 2 * 64 * -(-4 * K // 64) * M
+    out = {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
+           "layout": "[n, K] element-major" if layout_kind == "elem" else "[K, n] rows",
+           "K_local": K, "K_total": K * coll.world, "p": p, "selected": M, "alg_bytes": alg,
+           "alg_GBps": round(alg / t / 1e9, 1), "sector_bytes": sect, "sector_GBps": round(sect / t / 1e9, 1),
+           "sector_over_alg": round(sect / max(alg, 1), 3),
+           "path": "fused select+gather+average+write-back" if coll.world == 1 else
+                   f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter"}
+    if kern is not None:
+        out["kernel_ms"] = round(kern, 4)
+    if conv_ms is not None:
+        out["rows_to_elem_transpose_ms"] = round(conv_ms, 3)
+    return out
 
 
 def bench_simple(args, coll, dev, K_total=8, model="gpt2-char"):
@@ -425,7 +464,7 @@ def main():
     if single and not args.no_cpu_baseline and args.only is None:
         cpu = cpu_baseline_diloco(args.model, args.replicas)
     args.pmc = (None, "not measured (N > 1 or --no-pmc)")
-    if single and not args.no_pmc and args.only is None:
+    if single and not args.no_pmc and args.only is None and not under_profiler():
         args.pmc = pmc_traffic_live(args)
 
     coll = setup_dist(args.gpus)
@@ -443,7 +482,9 @@ def main():
     head = bench_diloco(args, coll, dev)
     extras = {}
     if not args.no_extras and args.only != "diloco":
-        runs = [("sparta_k32", bench_sparta), ("simple_reduce_char_k8", bench_simple),
+        runs = [("sparta_k32", bench_sparta),
+                ("sparta_k32_rows", lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows")),
+                ("simple_reduce_char_k8", bench_simple),
                 ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
         if coll.world > 1:  # configs[2] as named: one node per GPU, the exchange alone over xGMI
             def diloco_1(a, c, d):

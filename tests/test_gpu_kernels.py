@@ -462,9 +462,10 @@ def test_demo_encode_decode_matches_oracle(K, wave):
         np.testing.assert_allclose(gP[0, off:off + nel].reshape(shape)[ok], want_p[ok], rtol=0, atol=1e-6)
         for k in range(1, K):
             assert np.array_equal(gP[k, off:off + nel], gP[0, off:off + nel])
-    # a near-tied chunk is excluded whole (64x64 = 25% of a 128x128 tensor), so on
-    # these few-chunk tensors the floor is lower than at full size (test_gpu_fullsize)
-    tally.done(min_firm=0.9)
+    # a near-tied chunk is excluded whole (one 64x64 chunk = 13% of these ~31.7k
+    # elements; K=3 gives 3x the chances), so on these few-chunk tensors the floor
+    # is lower than at full size (test_gpu_fullsize)
+    tally.done(min_firm=0.8)
     # padding between tensors stays exactly zero in every arena
     for arr in (gP, gD, gS):
         for o, nel, o2 in zip(L.offsets, L.numels, L.offsets[1:] + [L.n]):

@@ -1,0 +1,119 @@
+"""Launch ONE kernel family of the bench's workloads repeatedly, nothing else on
+the GPU between launches (so a rocprofv3 --pmc pass attributes its counters to
+exactly that kernel and configuration).
+
+Modes (BASELINE configs):
+  demo_encode   ga_demo_encode_sym, GPT-2 350M (configs[4]), the bench's codec regime
+  demo_decode1  ga_demo_decode_sym, 1 source (own payload), grad written
+  demo_decode8  ga_demo_decode_sym, 8 distinct gathered payloads (what every GPU runs at 8 nodes)
+  sparta_elem   ga_sparta_average_local, K=32 GPT-2 124M, [n, K] element-major (configs[3])
+  sparta_rows   the same on the [K, n] row layout
+  diloco        ga_diloco_outer, K=8 GPT-2 124M (configs[2])
+Prints the HIP-event mean per launch and the algorithmic bytes per launch as one JSON line.
+Usage: python tools/prof_kernels.py <mode> [launches]"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from gym_amd import ops  # noqa: E402
+from gym_amd.arena import ArenaLayout  # noqa: E402
+from gym_amd.demo_codec import DemoPlan  # noqa: E402
+from gym_amd.shapes import MODELS, numel  # noqa: E402
+
+
+def timed(fn, launches):
+    fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / launches
+
+
+def synth(layout, K, dev, seed=1234):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    x = torch.zeros(K, layout.n, device=dev)
+    for o, n in zip(layout.offsets, layout.numels):
+        x[:, o:o + n].normal_(0.0, 0.02, generator=g)
+    return x
+
+
+def main():
+    mode = sys.argv[1]
+    launches = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(0)
+    out = {"mode": mode, "launches": launches}
+    if mode.startswith("demo"):
+        layout = ArenaLayout(MODELS["gpt2-350m"]())
+        plan = DemoPlan(layout).to(dev)
+        n = numel(MODELS["gpt2-350m"]())
+        P = synth(layout, 1, dev)
+        G = synth(layout, 1, dev, 7) * 0.05
+        D = torch.zeros_like(P)
+        pl = torch.zeros(1, 2 * plan.M, dtype=torch.int32, device=dev)
+        for _ in range(3):  # the bench's codec regime: a few whole steps first
+            ops.demo_encode(plan, P, G, D, pl, 1e-3, 0.999, 1.0)
+            ops.demo_decode(plan, pl, P, G, 1e-3)
+        if mode == "demo_encode":
+            ms = timed(lambda: ops.demo_encode(plan, P, G, D, pl, 1e-3, 0.999, 1.0), launches)
+            alg = 12 * n + 8 * plan.M
+        else:
+            S = 1 if mode == "demo_decode1" else 8
+            if S == 1:
+                gathered = pl
+            else:  # S distinct payloads: S nodes' encodes of independent deltas
+                gathered = torch.zeros(S, 2 * plan.M, dtype=torch.int32, device=dev)
+                for s in range(S):
+                    Ds = synth(layout, 1, dev, 100 + s) * 1e-4
+                    ops.demo_encode(plan, P, G, Ds, gathered[s:s + 1], 1e-3, 0.999, 1.0)
+            P0 = P.clone()
+            ms = timed(lambda: ops.demo_decode(plan, gathered, P, G, 1e-3), launches)
+            P.copy_(P0)
+            alg = 12 * n + 8 * plan.M * S
+        out.update(model="gpt2-350m", n=n, M=plan.M)
+    elif mode.startswith("sparta"):
+        layout = ArenaLayout(MODELS["gpt2-124m"]())
+        K, p = 32, 0.005
+        reps = synth(layout, K, dev)
+        kind = "elem" if mode == "sparta_elem" else "rows"
+        if kind == "elem":
+            reps = reps.t().contiguous()
+        it = [0]
+
+        def step():
+            ops.sparta_average_local(reps, layout.n, float(K), seed=42, iteration=it[0], p=p, layout=kind)
+            it[0] += 1
+
+        ms = timed(step, launches)
+        sel = int(round(layout.n * p))
+        alg = 2 * 4 * K * sel
+        out.update(model="gpt2-124m", K=K, p=p, layout=kind, selected_approx=sel)
+    elif mode == "diloco":
+        layout = ArenaLayout(MODELS["gpt2-124m"]())
+        K, n = 8, layout.n
+        reps = synth(layout, K, dev)
+        master = reps[0].clone()
+        mom = torch.zeros(n, device=dev)
+        ms = timed(lambda: ops.diloco_outer(reps, master, mom, reps, n, K, 0.7, 0.9, 0.0, 0.0, True, False),
+                   launches)
+        alg = (2 * K + 4) * 4 * n
+        out.update(model="gpt2-124m", K=K)
+    else:
+        raise SystemExit(f"unknown mode {mode}")
+    torch.cuda.synchronize()
+    out.update(ms=round(ms, 4), alg_bytes=alg, alg_GBps=round(alg / (ms * 1e-3) / 1e9, 1))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
