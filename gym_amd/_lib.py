@@ -51,11 +51,11 @@ SIGNATURES = {
     "ga_diloco_outer": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_i32, c_i32, c_f32, c_f32,
                                 c_f32, c_f32, c_i32, c_p, c_i64, c_i64, c_p]),
     "ga_sparta_workspace_bytes": (c_i64, [c_i64]),
-    "ga_sparta_threshold": (c_u32, [c_f64]),
-    "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_u32, c_p, c_i64, c_i64,
+    "ga_sparta_gap_table": (None, [c_f64, c_p]),
+    "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_f64, c_p, c_i64, c_i64,
                                  c_p, c_p, c_p, c_p, c_p]),
     "ga_sparta_scatter": (c_i32, [c_i32, c_p, c_p, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_i32, c_p]),
-    "ga_sparta_average_local": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_u32, c_p, c_i64,
+    "ga_sparta_average_local": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_f64, c_p, c_i64,
                                         c_f32, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "ga_demo_tensor_bytes": (c_i32, []),
     "ga_demo_encode": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32,

@@ -5,19 +5,31 @@
 // Selection is a stream compaction in ascending element order, so the packed
 // order equals `param.data[mask]` over the concatenated parameters
 // (sparta.py:38).  The mask is either a uint8 arena (rank 0's mask, exactly
-// the reference semantics) or generated in-kernel by Philox4x32-10 keyed by
-// (seed, iteration) — then every rank derives the same mask and nothing is
+// the reference semantics) or generated in-kernel from Philox4x32-10 keyed by
+// (seed, iteration) -- then every rank derives the same mask and nothing is
 // broadcast.  Three passes: per-tile count, one-block scan of tile counts,
-// select+gather (the predicate is recomputed; Philox is ~40 integer ops per
-// 4 elements, far below the HBM time of the gather).
+// select+gather (the predicate is recomputed).
+//
+// The Philox stream draws i.i.d. Bernoulli(p) selections as geometric gaps:
+// each 64-element group g takes the 32-bit words of
+// philox(key = seed, ctr = {g, r, iteration}) (r = 0, 1, ... as needed) in
+// order; a word u gives the gap t = #{j : T[j] <= u} to the next selected
+// element, where T[j] = round(2^32 (1 - (1 - p)^(j + 1))) (so P(gap = t) =
+// (1 - p)^t p up to the 2^-32 rounding), and u >= T[63] ends the group.  At
+// p = 0.005 a group costs one Philox call (~1.3 words) instead of sixteen
+// (one 24-bit draw per element): the mask no longer bounds the kernel.
+#include <math.h>
+
 #include "ga_common.h"
 
 namespace ga {
 
 constexpr int kSpBlock = 256;
-constexpr int kSpPerThread = 16;                       // elements per lane
-constexpr int kSpTile = kSpBlock * kSpPerThread;       // 4096 elements per workgroup
+constexpr int kSpPerThread = 64;                       // elements per lane: one Philox group
+constexpr int kSpTile = kSpBlock * kSpPerThread;       // 16384 elements per workgroup
+constexpr int kSelCap = 4096;                          // selected positions listed per window
 constexpr int kScanBlock = 1024;
+constexpr int kGapTable = 64;
 
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
@@ -36,15 +48,16 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 struct Pred {
     const uint8_t* mask;  // null -> Philox
     uint2 key;
-    uint32_t it_lo, it_hi, thr;
+    uint32_t it_lo, it_hi;
     const int64_t* skip;  // Philox: sorted disjoint [lo, hi) element ranges never selected
     int32_t nskip;
+    uint64_t gap[kGapTable];  // T[j] (<= 2^32), nondecreasing
 };
 
-// Clear the bits of the 16 elements at e0 that fall in a skipped range
+// Clear the bits of the 64 elements at e0 that fall in a skipped range
 // (tensors without a gradient, sparta.py:29-30).  Binary search for the first
-// range ending after e0; a 16-element group meets at most a few ranges.
-__device__ __forceinline__ uint32_t clear_skipped(const Pred& P, int64_t e0, uint32_t bits) {
+// range ending after e0; a 64-element group meets at most a few ranges.
+__device__ __forceinline__ uint64_t clear_skipped(const Pred& P, int64_t e0, uint64_t bits) {
     int lo = 0, hi = P.nskip;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -53,43 +66,74 @@ __device__ __forceinline__ uint32_t clear_skipped(const Pred& P, int64_t e0, uin
     }
     for (int r = lo; r < P.nskip && bits; ++r) {
         const int64_t a = P.skip[2 * r], b = P.skip[2 * r + 1];
-        if (a >= e0 + 16) break;
+        if (a >= e0 + 64) break;
         const int s = a > e0 ? (int)(a - e0) : 0;
-        const int t = b < e0 + 16 ? (int)(b - e0) : 16;
-        bits &= ~(((1u << t) - 1u) & ~((1u << s) - 1u));
+        const int t = b < e0 + 64 ? (int)(b - e0) : 64;
+        const uint64_t hi_m = t >= 64 ? ~0ull : ((1ull << t) - 1ull);
+        bits &= ~(hi_m & ~((1ull << s) - 1ull));
     }
     return bits;
 }
 
-// Selection bits of the 16 elements starting at element `e0` (e0 % 16 == 0).
-__device__ __forceinline__ uint32_t pred_bits16(const Pred& P, int64_t e0, int64_t n) {
-    uint32_t bits = 0;
+// gap of word u (< T[63]): the number of table entries <= u, by binary search
+__device__ __forceinline__ int gap_of(const uint64_t* tab, uint32_t u) {
+    int t = 0;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1)
+        if (tab[t + s - 1] <= (uint64_t)u) t += s;
+    return t;
+}
+
+// Selection bits of the 64 elements starting at element `e0` (e0 % 64 == 0);
+// tab: the gap table in LDS.
+__device__ __forceinline__ uint64_t pred_bits64(const Pred& P, const uint64_t* tab, int64_t e0, int64_t n) {
+    uint64_t bits = 0;
     if (P.mask) {
-        if (e0 + 16 <= n) {
-            const uint4 m = *reinterpret_cast<const uint4*>(P.mask + e0);
-            const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+        if (e0 + 64 <= n) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int v = 0; v < 4; ++v) {
+                const uint4 m = *reinterpret_cast<const uint4*>(P.mask + e0 + 16 * v);
+                const uint32_t w[4] = {m.x, m.y, m.z, m.w};
 #pragma unroll
-                for (int b = 0; b < 4; ++b) bits |= (((w[q] >> (8 * b)) & 0xffu) != 0u) << (4 * q + b);
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        bits |= (uint64_t)(((w[q] >> (8 * b)) & 0xffu) != 0u) << (16 * v + 4 * q + b);
+            }
         } else {
-            for (int j = 0; j < 16 && e0 + j < n; ++j) bits |= (P.mask[e0 + j] != 0) << j;
+            for (int j = 0; j < 64 && e0 + j < n; ++j) bits |= (uint64_t)(P.mask[e0 + j] != 0) << j;
         }
-    } else {
-        const uint64_t q0 = (uint64_t)e0 >> 2;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint64_t ctr = q0 + q;
-            const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), P.it_lo, P.it_hi), P.key);
-            bits |= ((r.x >> 8) < P.thr) << (4 * q + 0);
-            bits |= ((r.y >> 8) < P.thr) << (4 * q + 1);
-            bits |= ((r.z >> 8) < P.thr) << (4 * q + 2);
-            bits |= ((r.w >> 8) < P.thr) << (4 * q + 3);
-        }
-        if (e0 + 16 > n) bits &= (n - e0) >= 16 ? 0xffffu : ((1u << (uint32_t)(n - e0)) - 1u);
-        if (P.nskip) bits = clear_skipped(P, e0, bits);
+        return bits;
     }
+    const uint64_t t63 = tab[kGapTable - 1];
+    const uint32_t g = (uint32_t)(e0 >> 6);  // n < 2^31: g < 2^25
+    int pos = 0;
+    bool live = true;
+    for (uint32_t r = 0; live; ++r) {
+        const uint4 w4 = philox4x32_10(make_uint4(g, r, P.it_lo, P.it_hi), P.key);
+        const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (live) {
+                if ((uint64_t)w[j] >= t63) {
+                    live = false;
+                } else {
+                    pos += gap_of(tab, w[j]);
+                    if (pos < 64) bits |= 1ull << pos;
+                    ++pos;
+                    live = pos < 64;
+                }
+            }
+        }
+    }
+    if (e0 + 64 > n) bits &= (n - e0) >= 64 ? ~0ull : ((1ull << (uint32_t)(n - e0)) - 1ull);
+    if (P.nskip) bits = clear_skipped(P, e0, bits);
     return bits;
+}
+
+__device__ __forceinline__ void load_gap_table(const Pred& P, uint64_t* tab) {
+    if (threadIdx.x < kGapTable) tab[threadIdx.x] = P.gap[threadIdx.x];
+    __syncthreads();
 }
 
 // Exclusive scan of one int per lane over a 256-lane workgroup.
@@ -117,8 +161,10 @@ __device__ __forceinline__ int block_excl_scan_256(int v, int* wave_tot, int* to
 
 __global__ __launch_bounds__(kSpBlock) void sparta_count_kernel(Pred P, int64_t n, int32_t* tile_counts) {
     __shared__ int wave_tot[4];
+    __shared__ uint64_t tab[kGapTable];
+    load_gap_table(P, tab);
     const int64_t e0 = (int64_t)blockIdx.x * kSpTile + (int64_t)threadIdx.x * kSpPerThread;
-    const int c = e0 < n ? __popc(pred_bits16(P, e0, n)) : 0;
+    const int c = e0 < n ? __popcll(pred_bits64(P, tab, e0, n)) : 0;
     int total;
     block_excl_scan_256(c, wave_tot, &total);
     if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
@@ -179,6 +225,14 @@ __global__ __launch_bounds__(kScanBlock) void sparta_scan_kernel(const int32_t* 
     }
 }
 
+// Exact unsigned division of small numerators (f * d < 2^32) by a uniform d.
+struct FastDiv {
+    uint64_t m;  // ceil(2^32 / d)
+    uint32_t d;
+    __device__ __forceinline__ explicit FastDiv(uint32_t dd) : m(((1ull << 32) + dd - 1) / dd), d(dd) {}
+    __device__ __forceinline__ uint32_t div(uint32_t f) const { return (uint32_t)(((uint64_t)f * m) >> 32); }
+};
+
 // Select + gather.  The workgroup recomputes its tile's predicate, scans it
 // to output positions, lists its selected elements in LDS, then all 256 lanes
 // load the (element, replica) pairs densely (one load per lane, no idle lanes
@@ -210,81 +264,102 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
                                                                  int64_t cap, int32_t* __restrict__ idx,
                                                                  T* __restrict__ vals, float divisor) {
     __shared__ int wave_tot[4];
-    __shared__ uint16_t sel_list[kSpTile];  // tile-local positions (< 4096)
+    __shared__ uint64_t tab[kGapTable];
+    __shared__ uint16_t sel_list[kSelCap];  // tile-local positions (< 16384) of one window
     __shared__ float gv[kGatherSlots];
     __shared__ float gavg[kSpBlock];
+    load_gap_table(P, tab);
     const int64_t tile0 = (int64_t)blockIdx.x * kSpTile;
     const int64_t e0 = tile0 + (int64_t)threadIdx.x * kSpPerThread;
-    uint32_t bits = e0 < n ? pred_bits16(P, e0, n) : 0u;
+    const uint64_t bits0 = e0 < n ? pred_bits64(P, tab, e0, n) : 0ull;
     int total;
-    int local = block_excl_scan_256(__popc(bits), wave_tot, &total);
+    const int local0 = block_excl_scan_256(__popcll(bits0), wave_tot, &total);
     const int64_t out0 = tile_offsets ? tile_offsets[blockIdx.x] : 0;
-    while (bits) {
-        const int j = __ffs(bits) - 1;
-        bits &= bits - 1;
-        const int32_t i = (int32_t)(threadIdx.x * kSpPerThread + j);
-        sel_list[local] = (uint16_t)i;
-        const int64_t pos = out0 + local;
-        if (idx && pos < cap) idx[pos] = (int32_t)(tile0 + i);
-        ++local;
-    }
-    __syncthreads();
-    // entries per pass: as many as fit K values each in the LDS slots
-    const int per_pass = K >= kGatherSlots ? 1 : (kGatherSlots / K < kSpBlock ? kGatherSlots / (int)K : kSpBlock);
+    // entries per pass: as many as fit K values each in the LDS slots.  An
+    // entry's K values sit at an odd LDS stride Kp (K, or K + 1 for even K), so
+    // lanes of consecutive entries (the rows layout's stores, every layout's
+    // per-entry sums) hit distinct banks instead of one bank at K = 32.
     const int Ki = (int)(K < kGatherSlots ? K : kGatherSlots);
-    for (int c0 = 0; c0 < total; c0 += per_pass) {
-        const int ce = (total - c0) < per_pass ? (total - c0) : per_pass;
-        if (K <= kGatherSlots) {
-            // lane f -> (element e, replica k): replica-major for [K, ld] rows,
-            // element-major for [n, ld] (one element's replicas on adjacent lanes)
-            // every lane's loads of the pass issued back to back (one HBM latency
-            // per pass instead of one per load), then staged into LDS
-            constexpr int kLoads = kGatherSlots / kSpBlock;
-            float v[kLoads];
-#pragma unroll
-            for (int u = 0; u < kLoads; ++u) {
-                const int f = threadIdx.x + u * kSpBlock;
-                if (f < ce * Ki) {
-                    const int k = R.em ? f % Ki : f / ce, e = R.em ? f / Ki : f - k * ce;
-                    v[u] = Elem<T>::load(src + R.at(tile0 + sel_list[c0 + e], k));
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kLoads; ++u) {
-                const int f = threadIdx.x + u * kSpBlock;
-                if (f < ce * Ki) {
-                    const int k = R.em ? f % Ki : f / ce, e = R.em ? f / Ki : f - k * ce;
-                    gv[e * Ki + k] = v[u];
-                }
-            }
-            __syncthreads();
-            if (threadIdx.x < ce) {
-                float acc = 0.f;
-                for (int64_t k = 0; k < K; ++k) acc += gv[threadIdx.x * K + k];
-                const int64_t pos = out0 + c0 + threadIdx.x;
-                if (vals && pos < cap) Elem<T>::store(vals + pos, acc);
-                if (divisor > 0.f) gavg[threadIdx.x] = acc / divisor;
-            }
-            __syncthreads();
-            if (divisor > 0.f) {
-                for (int f = threadIdx.x; f < ce * Ki; f += kSpBlock) {
-                    const int k = R.em ? f % Ki : f / ce, e = R.em ? f / Ki : f - k * ce;
-                    Elem<T>::store(src + R.at(tile0 + sel_list[c0 + e], k), gavg[e]);
-                }
-                __syncthreads();
-            }
-        } else {  // very many replicas: one element at a time, lanes over replicas
-            const int64_t i = tile0 + sel_list[c0];
-            float acc = 0.f;
-            if (threadIdx.x == 0)
-                for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + R.at(i, k));
-            const int64_t pos = out0 + c0;
-            if (threadIdx.x == 0 && vals && pos < cap) Elem<T>::store(vals + pos, acc);
-            if (threadIdx.x == 0 && divisor > 0.f) {
-                const float a = acc / divisor;
-                for (int64_t k = 0; k < K; ++k) Elem<T>::store(src + R.at(i, k), a);
+    const int Kp = (Ki & 1) || Ki + 1 > kGatherSlots ? Ki : Ki + 1;
+    const int per_pass = K >= kGatherSlots ? 1 : (kGatherSlots / Kp < kSpBlock ? kGatherSlots / Kp : kSpBlock);
+    const FastDiv divK((uint32_t)Ki);
+    // the tile's selected elements in windows of kSelCap list slots (one window
+    // unless p is large)
+    for (int w0 = 0; w0 < total; w0 += kSelCap) {
+        {
+            uint64_t bits = bits0;
+            int local = local0;
+            while (bits) {
+                const int j = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                const int32_t i = (int32_t)(threadIdx.x * kSpPerThread + j);
+                if (local >= w0 && local < w0 + kSelCap) sel_list[local - w0] = (uint16_t)i;
+                const int64_t pos = out0 + local;
+                if (w0 == 0 && idx && pos < cap) idx[pos] = (int32_t)(tile0 + i);
+                ++local;
             }
         }
+        __syncthreads();
+        const int wtot = (total - w0) < kSelCap ? (total - w0) : kSelCap;
+        for (int c0 = 0; c0 < wtot; c0 += per_pass) {
+            const int ce = (wtot - c0) < per_pass ? (wtot - c0) : per_pass;
+            if (K <= kGatherSlots) {
+                // lane f -> (element e, replica k): replica-major for [K, ld] rows,
+                // element-major for [n, ld] (one element's replicas on adjacent lanes)
+                // every lane's loads of the pass issued back to back (one HBM latency
+                // per pass instead of one per load), then staged into LDS
+                const FastDiv divC((uint32_t)ce);
+                constexpr int kLoads = kGatherSlots / kSpBlock;
+                float v[kLoads];
+#pragma unroll
+                for (int u = 0; u < kLoads; ++u) {
+                    const int f = threadIdx.x + u * kSpBlock;
+                    if (f < ce * Ki) {
+                        const int k = R.em ? f - (int)divK.div(f) * Ki : (int)divC.div(f);
+                        const int e = R.em ? (int)divK.div(f) : f - k * ce;
+                        v[u] = Elem<T>::load(src + R.at(tile0 + sel_list[c0 + e], k));
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kLoads; ++u) {
+                    const int f = threadIdx.x + u * kSpBlock;
+                    if (f < ce * Ki) {
+                        const int k = R.em ? f - (int)divK.div(f) * Ki : (int)divC.div(f);
+                        const int e = R.em ? (int)divK.div(f) : f - k * ce;
+                        gv[e * Kp + k] = v[u];
+                    }
+                }
+                __syncthreads();
+                if (threadIdx.x < ce) {
+                    float acc = 0.f;
+                    for (int k = 0; k < Ki; ++k) acc += gv[threadIdx.x * Kp + k];
+                    const int64_t pos = out0 + w0 + c0 + threadIdx.x;
+                    if (vals && pos < cap) Elem<T>::store(vals + pos, acc);
+                    if (divisor > 0.f) gavg[threadIdx.x] = acc / divisor;
+                }
+                __syncthreads();
+                if (divisor > 0.f) {
+                    for (int f = threadIdx.x; f < ce * Ki; f += kSpBlock) {
+                        const int k = R.em ? f - (int)divK.div(f) * Ki : (int)divC.div(f);
+                        const int e = R.em ? (int)divK.div(f) : f - k * ce;
+                        Elem<T>::store(src + R.at(tile0 + sel_list[c0 + e], k), gavg[e]);
+                    }
+                    __syncthreads();
+                }
+            } else {  // very many replicas: one element at a time, lanes over replicas
+                const int64_t i = tile0 + sel_list[c0];
+                float acc = 0.f;
+                if (threadIdx.x == 0)
+                    for (int64_t k = 0; k < K; ++k) acc += Elem<T>::load(src + R.at(i, k));
+                const int64_t pos = out0 + w0 + c0;
+                if (threadIdx.x == 0 && vals && pos < cap) Elem<T>::store(vals + pos, acc);
+                if (threadIdx.x == 0 && divisor > 0.f) {
+                    const float a = acc / divisor;
+                    for (int64_t k = 0; k < K; ++k) Elem<T>::store(src + R.at(i, k), a);
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -351,18 +426,34 @@ extern "C" GA_API int64_t ga_sparta_workspace_bytes(int64_t n) {
     return 2 * sparta_tiles(n < 0 ? 0 : n) * (int64_t)sizeof(int32_t) + 256;
 }
 
-extern "C" GA_API uint32_t ga_sparta_threshold(double p) {
-    if (!(p > 0.0)) return 0u;
-    if (p >= 1.0) return 1u << 24;
-    double t = p * 16777216.0;
-    uint32_t u = (uint32_t)t;
-    if ((double)u < t) ++u;  // ceil
-    return u;
+extern "C" GA_API void ga_sparta_gap_table(double p, uint64_t* table) {
+    // T[j] = round(2^32 * P(gap <= j)), P(gap <= j) = 1 - (1 - p)^(j + 1) = -expm1((j + 1) log1p(-p))
+    for (int j = 0; j < kGapTable; ++j) {
+        double v;
+        if (!(p > 0.0)) v = 0.0;
+        else if (p >= 1.0) v = 4294967296.0;
+        else v = floor(-expm1((double)(j + 1) * log1p(-p)) * 4294967296.0 + 0.5);
+        if (v > 4294967296.0) v = 4294967296.0;
+        table[j] = (uint64_t)v;
+    }
+}
+
+static Pred make_pred(const uint8_t* mask, uint64_t seed, uint64_t iteration, double p, const int64_t* skip,
+                      int64_t nskip) {
+    Pred P;
+    P.mask = mask;
+    P.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+    P.it_lo = (uint32_t)iteration;
+    P.it_hi = (uint32_t)(iteration >> 32);
+    P.skip = skip;
+    P.nskip = (int32_t)nskip;
+    ga_sparta_gap_table(mask ? 0.0 : p, P.gap);
+    return P;
 }
 
 extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld, int layout, int64_t n,
                                        const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                       uint32_t threshold, const int64_t* skip, int64_t nskip,
+                                       double p, const int64_t* skip, int64_t nskip,
                                        int64_t cap, int32_t* idx, void* vals,
                                        int64_t* count, void* work, hipStream_t stream) {
     clear_error();
@@ -371,19 +462,12 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     GA_REQUIRE(count && work, "ga_sparta_select: null count/work");
     GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_select: bad layout %d", layout);
     GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_select: ld too small");
-    GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_select: threshold > 2^24");
+    GA_REQUIRE(p >= 0.0 && p <= 1.0, "ga_sparta_select: p=%g outside [0, 1]", p);
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_select: mask must be 16-byte aligned");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_select: bad skip table");
     if (n == 0) return hipMemsetAsync(count, 0, 2 * sizeof(int64_t), stream) == hipSuccess ? GA_OK : GA_EHIP;
     GA_REQUIRE(src && idx && vals, "ga_sparta_select: null src/idx/vals");
-    Pred P;
-    P.mask = mask;
-    P.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-    P.it_lo = (uint32_t)iteration;
-    P.it_hi = (uint32_t)(iteration >> 32);
-    P.thr = threshold;
-    P.skip = skip;
-    P.nskip = (int32_t)nskip;
+    const Pred P = make_pred(mask, seed, iteration, p, skip, nskip);
     switch (dtype) {
         case GA_F32:
             return launch_select<float>(src, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work, 0.f, stream);
@@ -396,7 +480,7 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
 
 extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int layout, int64_t n,
                                               const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                              uint32_t threshold, const int64_t* skip, int64_t nskip,
+                                              double p, const int64_t* skip, int64_t nskip,
                                               float divisor, int32_t* idx, void* vals,
                                               int64_t cap, int64_t* count, void* work, hipStream_t stream) {
     clear_error();
@@ -405,21 +489,14 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
     GA_REQUIRE(divisor > 0.0f, "ga_sparta_average_local: divisor must be > 0");
     GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_average_local: bad layout");
     GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_average_local: ld too small");
-    GA_REQUIRE(threshold <= (1u << 24), "ga_sparta_average_local: threshold > 2^24");
+    GA_REQUIRE(p >= 0.0 && p <= 1.0, "ga_sparta_average_local: p=%g outside [0, 1]", p);
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_average_local: mask alignment");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_average_local: bad skip table");
     GA_REQUIRE((idx == nullptr && vals == nullptr && count == nullptr) || (idx && vals && count && work),
                "ga_sparta_average_local: idx, vals, count and work go together");
     if (n == 0) return GA_OK;
     GA_REQUIRE(reps, "ga_sparta_average_local: null replicas");
-    Pred P;
-    P.mask = mask;
-    P.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-    P.it_lo = (uint32_t)iteration;
-    P.it_hi = (uint32_t)(iteration >> 32);
-    P.thr = threshold;
-    P.skip = skip;
-    P.nskip = (int32_t)nskip;
+    const Pred P = make_pred(mask, seed, iteration, p, skip, nskip);
     switch (dtype) {
         case GA_F32:
             return launch_select<float>(reps, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work, divisor,

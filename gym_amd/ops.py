@@ -97,8 +97,21 @@ def diloco_outer(src, master, mom, dst, n, divisor, lr, momentum, dampening, wei
           "ga_diloco_outer")
 
 
-def sparta_threshold(p):
-    return int(lib().ga_sparta_threshold(float(p)))
+def sparta_gap_table(p):
+    """The 64-entry gap table of the Philox mask stream (include/gym_amd.h)."""
+    import ctypes
+    buf = (ctypes.c_uint64 * 64)()
+    lib().ga_sparta_gap_table(float(p), buf)
+    return [int(v) for v in buf]
+
+
+def _rate(p, mask):
+    if mask is not None:
+        return 0.0
+    p = float(p)
+    if not 0.0 <= p <= 1.0:
+        raise ValueError(f"SPARTA selection rate p={p} outside [0, 1]")
+    return p
 
 
 def sparta_workspace(n, device):
@@ -153,7 +166,7 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
     if mask is not None:
         if mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n:
             raise ValueError("sparta_select: mask must be uint8/bool with >= n elements")
-    thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
+    thr = _rate(p, mask)
     check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, code, int(n), _p(mask), int(seed) & (2**64 - 1),
                                  int(iteration) & (2**64 - 1), thr, _p(skip), nskip, int(cap), _p(idx), _p(vals),
                                  _p(count),
@@ -177,7 +190,7 @@ def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0
             raise TypeError("sparta_average_local: idx int32, vals arena dtype, count int64")
         if idx.numel() < cap or vals.numel() < cap or work.numel() < lib().ga_sparta_workspace_bytes(int(n)):
             raise ValueError("sparta_average_local: output buffers too small")
-    thr = lib().ga_sparta_threshold(float(p)) if mask is None else 0
+    thr = _rate(p, mask)
     check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, code, int(n), _p(mask),
                                         int(seed) & (2**64 - 1),
                                         int(iteration) & (2**64 - 1), thr, _p(skip), nskip, float(divisor),

@@ -111,8 +111,18 @@ GA_API int ga_diloco_outer(int dtype, const void* src, int64_t K, int64_t ld_src
 /* Workspace bytes needed by ga_sparta_select for an arena of n elements. */
 GA_API int64_t ga_sparta_workspace_bytes(int64_t n);
 
-/* Selection threshold used by the Philox mask: select iff (u32 >> 8) < thr. */
-GA_API uint32_t ga_sparta_threshold(double p);
+/*
+ * Gap table of the Philox mask stream for selection rate p (64 entries):
+ * table[j] = round(2^32 * (1 - (1 - p)^(j + 1))) (0 for p <= 0, 2^32 for
+ * p >= 1), nondecreasing.  Each 64-element group g of the arena reads the
+ * 32-bit words of philox4x32_10(key = seed, ctr = {g, r, iteration_lo,
+ * iteration_hi}), r = 0, 1, ..., in order (x, y, z, w); starting at pos = 0,
+ * a word u >= table[63] ends the group, otherwise pos += #{j : table[j] <= u},
+ * element 64 g + pos is selected if pos < 64, and pos += 1 (the group ends at
+ * pos >= 64).  The gaps are Geometric(p): every element is selected
+ * independently with probability p (up to the 2^-32 rounding of the table).
+ */
+GA_API void ga_sparta_gap_table(double p, uint64_t* table);
 
 /*
  * Select the SPARTA index set over an arena of n elements and gather the
@@ -120,9 +130,8 @@ GA_API uint32_t ga_sparta_threshold(double p);
  * GA_LAYOUT_*).
  *   mask source: if mask != null, element i is selected iff mask[i] != 0
  *   (uint8 mask arena: rank 0's per-tensor index_selector masks, broadcast --
- *   sparta.py:32-37); otherwise the in-kernel Philox4x32-10 stream decides:
- *   select iff (philox(key=seed, ctr={i/4, iteration})[i%4] >> 8) < threshold,
- *   except inside the `nskip` element ranges skip[2r] <= i < skip[2r+1]
+ *   sparta.py:32-37); otherwise the in-kernel Philox4x32-10 stream decides
+ *   with selection rate p (see ga_sparta_gap_table), except inside the `nskip` element ranges skip[2r] <= i < skip[2r+1]
  *   (sorted, disjoint: the tensors without a gradient, which the reference
  *   skips, sparta.py:29-30; skip may be null when nskip == 0).
  * Outputs (device): idx[j] = j-th selected element index in ascending order
@@ -136,7 +145,7 @@ GA_API uint32_t ga_sparta_threshold(double p);
  */
 GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld,
                             int layout, int64_t n, const uint8_t* mask, uint64_t seed,
-                            uint64_t iteration, uint32_t threshold,
+                            uint64_t iteration, double p,
                             const int64_t* skip, int64_t nskip, int64_t cap,
                             int32_t* idx, void* vals, int64_t* count, void* work,
                             hipStream_t stream);
@@ -161,7 +170,7 @@ GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
  */
 GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int layout, int64_t n,
                                    const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                   uint32_t threshold, const int64_t* skip, int64_t nskip,
+                                   double p, const int64_t* skip, int64_t nskip,
                                    float divisor, int32_t* idx, void* vals,
                                    int64_t cap, int64_t* count, void* work, hipStream_t stream);
 

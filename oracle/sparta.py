@@ -12,9 +12,11 @@ Selectors restated given their torch random draws as inputs:
 
 gym_amd's fast mask mode has no reference counterpart: it draws the mask from
 Philox4x32-10 (Salmon et al., SC'11, "Parallel random numbers: as easy as
-1, 2, 3"; constants as in Random123) keyed by (seed, iteration) over the flat
-arena index.  `philox4x32_10` restates that generator; it is pinned by the
-Random123 known-answer vectors in tests/test_oracle_golden.py.
+1, 2, 3"; constants as in Random123) keyed by (seed, iteration), as the
+geometric gaps between selected elements of each 64-element group (one
+Bernoulli(p) draw per element in distribution; `philox_mask`).
+`philox4x32_10` restates that generator; it is pinned by the Random123
+known-answer vectors in tests/test_oracle_golden.py.
 """
 import math
 
@@ -48,30 +50,64 @@ def _philox_rounds(c, k0, k1):
     return np.stack(c, axis=-1)
 
 
-def threshold(p):
-    """Integer threshold: select iff (u32 >> 8) < threshold(p) (P = thr / 2^24)."""
-    if not p > 0.0:
-        return 0
-    if p >= 1.0:
-        return 1 << 24
-    return int(math.ceil(p * 16777216.0))
+GAP_TABLE = 64
+
+
+def gap_table(p):
+    """T[j] = round(2^32 (1 - (1 - p)^(j+1))) for j < 64 (include/gym_amd.h,
+    ga_sparta_gap_table): a 32-bit word u gives the gap #{j : T[j] <= u}."""
+    out = []
+    for j in range(GAP_TABLE):
+        if not p > 0.0:
+            v = 0.0
+        elif p >= 1.0:
+            v = 4294967296.0
+        else:
+            v = math.floor(-math.expm1((j + 1) * math.log1p(-p)) * 4294967296.0 + 0.5)
+        out.append(int(min(v, 4294967296.0)))
+    return np.array(out, dtype=np.uint64)
 
 
 def philox_mask(n, seed, iteration, p, start=0, skip=None):
-    """Mask bits of arena elements [start, start+n) for (seed, iteration);
-    elements inside a `skip` range [lo, hi) are never selected (tensors
-    without a gradient, which SparseCommunicator.communicate skips,
-    exogym/strategy/sparta.py:29-30)."""
-    idx = np.arange(start, start + n, dtype=np.uint64)
-    q = idx >> np.uint64(2)
-    ctr = np.stack([(q & MASK32).astype(np.uint32), (q >> np.uint64(32)).astype(np.uint32),
-                    np.full(n, iteration & 0xFFFFFFFF, np.uint32),
-                    np.full(n, (iteration >> 32) & 0xFFFFFFFF, np.uint32)], axis=-1)
+    """Mask bits of arena elements [start, start+n) for (seed, iteration):
+    i.i.d. Bernoulli(p) as geometric gaps -- group g = 64 elements reads the
+    words of philox(key=seed, ctr={g, r, iteration}), r = 0, 1, ..., in order;
+    u >= T[63] ends the group, else pos += #{j : T[j] <= u}, element 64g+pos is
+    selected (pos < 64), pos += 1.  Elements inside a `skip` range [lo, hi)
+    are never selected (tensors without a gradient, which
+    SparseCommunicator.communicate skips, exogym/strategy/sparta.py:29-30)."""
+    if n <= 0:
+        return np.zeros(0, dtype=bool)
+    tab = gap_table(p)
+    g0, g1 = start // 64, (start + n - 1) // 64 + 1
+    G = g1 - g0
+    groups = np.arange(g0, g1, dtype=np.uint64)
+    bits = np.zeros((G, 64), dtype=bool)
+    pos = np.zeros(G, dtype=np.int64)
+    live = np.ones(G, dtype=bool)
     key = np.array([seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF], dtype=np.uint32)
-    words = philox4x32_10(ctr, key)
-    lane = (idx & np.uint64(3)).astype(np.int64)
-    w = words[np.arange(n), lane]
-    m = (w >> np.uint32(8)) < np.uint32(threshold(p))
+    r = 0
+    while live.any():
+        act = np.flatnonzero(live)
+        ctr = np.stack([(groups[act] & MASK32).astype(np.uint32), np.full(act.size, r, np.uint32),
+                        np.full(act.size, iteration & 0xFFFFFFFF, np.uint32),
+                        np.full(act.size, (iteration >> 32) & 0xFFFFFFFF, np.uint32)], axis=-1)
+        words = philox4x32_10(ctr, key)
+        for j in range(4):
+            lv = live[act]
+            u = words[:, j].astype(np.uint64)
+            end = lv & (u >= tab[GAP_TABLE - 1])
+            live[act[end]] = False
+            go = lv & ~end
+            a = act[go]
+            gap = np.searchsorted(tab, u[go], side="right")  # #{j : T[j] <= u}
+            pos[a] += gap
+            sel = pos[a] < 64
+            bits[a[sel], pos[a[sel]]] = True
+            pos[a] += 1
+            live[a[pos[a] >= 64]] = False
+        r += 1
+    m = bits.reshape(-1)[start - 64 * g0: start - 64 * g0 + n].copy()
     for lo, hi in (skip if skip is not None else ()):
         a, b = max(int(lo) - start, 0), min(int(hi) - start, n)
         if a < b:

@@ -48,8 +48,8 @@ def diloco_outer(src, master, mom, dst, n, divisor, lr, momentum, dampening, wei
             d2[j, :n].copy_(torch.from_numpy(nm).to(d2.dtype))
 
 
-def sparta_threshold(p):
-    return osparta.threshold(p)
+def sparta_gap_table(p):
+    return [int(v) for v in osparta.gap_table(p)]
 
 
 def sparta_workspace(n, device):

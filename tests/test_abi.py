@@ -20,19 +20,26 @@ def test_exports_every_header_symbol():
 
 def test_version_and_struct_layout():
     L = _lib.lib()
-    assert L.ga_abi_version() == 100
+    assert L.ga_abi_version() == 101
     assert L.ga_demo_tensor_bytes() == ctypes.sizeof(_lib.DemoTensor) == 56
 
 
-def test_sparta_threshold_and_workspace():
+def test_sparta_gap_table_and_workspace():
+    """The library's gap table (host code, no GPU) equals the oracle's, entry
+    for entry, so the in-kernel Philox mask and oracle.sparta.philox_mask are
+    one stream."""
+    from gym_amd import ops
+    from oracle.sparta import gap_table
+    assert ops.sparta_gap_table(0.0) == [0] * 64
+    assert ops.sparta_gap_table(1.0) == [1 << 32] * 64
+    for p in (1e-9, 1e-7, 0.005, 0.01, 0.05, 0.3333, 0.5, 0.9, 0.9999999):
+        t = ops.sparta_gap_table(p)
+        assert t == [int(v) for v in gap_table(p)], p
+        assert all(a <= b for a, b in zip(t, t[1:])) and t[-1] <= 1 << 32
+    t = ops.sparta_gap_table(0.005)
+    assert abs(t[0] / 2 ** 32 - 0.005) < 1e-9  # P(gap = 0) = p
     L = _lib.lib()
-    assert L.ga_sparta_threshold(0.0) == 0
-    assert L.ga_sparta_threshold(1.0) == 1 << 24
-    assert L.ga_sparta_threshold(0.005) == 83887  # ceil(0.005 * 2^24)
-    from oracle.sparta import threshold
-    for p in (1e-7, 0.005, 0.05, 0.3333, 0.5, 0.9999999):
-        assert L.ga_sparta_threshold(p) == threshold(p)
-    assert L.ga_sparta_workspace_bytes(4096 * 10) >= 2 * 4 * 10
+    assert L.ga_sparta_workspace_bytes(16384 * 10) >= 2 * 4 * 10
 
 
 @pytest.mark.parametrize("call", [

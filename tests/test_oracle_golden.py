@@ -125,13 +125,51 @@ def test_philox_known_answers():
         assert [int(x) for x in got] == want
 
 
+def _walk_mask_scalar(n, seed, iteration, p):
+    """The gap stream restated one group and one word at a time (pins the
+    vectorised oracle.sparta.philox_mask)."""
+    tab = [int(v) for v in osparta.gap_table(p)]
+    out = np.zeros(n, dtype=bool)
+    key = np.array([seed & 0xFFFFFFFF, seed >> 32], np.uint32)
+    for g in range((n + 63) // 64):
+        pos, r, live = 0, 0, True
+        while live:
+            w = osparta.philox4x32_10(np.array([[g, r, iteration & 0xFFFFFFFF, iteration >> 32]], np.uint32), key)[0]
+            for u in (int(x) for x in w):
+                if not live:
+                    break
+                if u >= tab[63]:
+                    live = False
+                    break
+                pos += sum(1 for t in tab if t <= u)
+                if pos < 64 and 64 * g + pos < n:
+                    out[64 * g + pos] = True
+                pos += 1
+                live = pos < 64
+            r += 1
+    return out
+
+
 def test_philox_mask_rate():
     m = osparta.philox_mask(1 << 20, seed=123, iteration=7, p=0.005)
     rate = m.mean()
     assert abs(rate - 0.005) < 5 * np.sqrt(0.005 / (1 << 20))
-    # counters are per element: a window equals the same slice of a bigger draw
-    assert np.array_equal(osparta.philox_mask(1000, 123, 7, 0.3, start=4096),
-                          osparta.philox_mask(5096, 123, 7, 0.3)[4096:])
+    # gaps between selected elements are Geometric(p): mean (1-p)/p, P(gap=0) = p
+    m = osparta.philox_mask(1 << 22, seed=1, iteration=0, p=0.01)
+    gaps = np.diff(np.flatnonzero(m)) - 1
+    assert abs(gaps.mean() - 99.0) < 5 * np.sqrt(99.0 * 100.0 / gaps.size)
+    assert abs((gaps == 0).mean() - 0.01) < 5 * np.sqrt(0.01 / gaps.size)
+    # counters are per 64-element group: a window equals the same slice of a bigger draw
+    assert np.array_equal(osparta.philox_mask(1000, 123, 7, 0.3, start=4099),
+                          osparta.philox_mask(5099, 123, 7, 0.3)[4099:])
+    for p in (0.0, 1.0):
+        assert osparta.philox_mask(777, 3, 4, p).mean() == p
+
+
+@pytest.mark.parametrize("p", [0.005, 0.3, 0.97])
+def test_philox_mask_matches_scalar_walk(p):
+    n = 64 * 40 + 17
+    assert np.array_equal(osparta.philox_mask(n, 99, (5 << 32) + 3, p), _walk_mask_scalar(n, 99, (5 << 32) + 3, p))
 
 
 # ---- G4 DeMo codec ----------------------------------------------------------

@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc counter CSVs per kernel (median over dispatches).
 
 Usage: python tools/pmc_kernels.py <counter_collection.csv or glob> [name-substring ...]
+       python tools/pmc_kernels.py --filter <rocprofv3 output dir> name-substring ...
 Several passes (one CSV each, e.g. "out/mode_p*/run_counter_collection.csv")
 are merged per kernel name.  Prints, per kernel whose name matches, the median
 of every collected counter over its dispatches and the derived figures the
@@ -38,7 +39,30 @@ def load(paths, pats):
     return vals, meta
 
 
+def filter_dir(d, pats):
+    """Keep only the rows of kernels matching pats in d's counter CSVs and drop
+    every other rocprofv3 output file (keeps gpurun_out/ small)."""
+    import os
+    for root, _, files in os.walk(d):
+        for f in files:
+            path = os.path.join(root, f)
+            if not f.endswith("counter_collection.csv"):
+                os.remove(path)
+                continue
+            with open(path) as fh:
+                rows = list(csv.reader(fh))
+            head, body = rows[0], rows[1:]
+            ki = head.index("Kernel_Name")
+            with open(path, "w", newline="") as fh:
+                w = csv.writer(fh, quoting=csv.QUOTE_MINIMAL)
+                w.writerow(head)
+                w.writerows(r for r in body if any(p in r[ki] for p in pats))
+
+
 def main():
+    if sys.argv[1] == "--filter":
+        filter_dir(sys.argv[2], sys.argv[3:])
+        return
     paths = []
     for a in sys.argv[1:2]:
         paths += sorted(glob.glob(a)) if any(c in a for c in "*?[") else [a]

@@ -24,6 +24,7 @@ for MODE in "$@"; do
   for P in "${PASSES[@]}"; do
     D=$O/${MODE}_p$i
     timeout -s KILL 120 rocprofv3 --pmc $P -d $D -o run --output-format csv -- python3 tools/prof_kernels.py $MODE 5 > $D.log 2>&1 || { echo "PMC $MODE pass $i FAILED"; tail -20 $D.log; exit 1; }
+    python3 tools/pmc_kernels.py --filter $D ga:: || { echo "FILTER $MODE FAILED"; exit 1; }
     i=$((i+1))
   done
   python3 tools/pmc_kernels.py "$O/${MODE}_p*/run_counter_collection.csv" ga:: > $O/${MODE}_pmc.txt 2>&1 || echo "SUMMARY $MODE FAILED"
