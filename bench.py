@@ -326,6 +326,7 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     # replica) is a random 4-B word = one 64-B read sector + one 32-B write sector;
     # elem -> one element's K values are ceil(4K/64) whole 64-B sectors each way
     sect = (64 + 32) * K * M if layout_kind == "rows" else 2 * 64 * -(-4 * K // 64) * M
+    sect += 8 * M if coll.world > 1 else 0  # the packed idx/vals list
     out = {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
            "layout": "[n, K] element-major" if layout_kind == "elem" else "[K, n] rows",
            "K_local": K, "K_total": K * coll.world, "p": p, "selected": M, "alg_bytes": alg,

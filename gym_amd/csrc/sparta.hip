@@ -27,7 +27,10 @@ namespace ga {
 constexpr int kSpBlock = 256;
 constexpr int kSpPerThread = 64;                       // elements per lane: one Philox group
 constexpr int kSpTile = kSpBlock * kSpPerThread;       // 16384 elements per workgroup
-constexpr int kSelCap = 4096;                          // selected positions listed per window
+#ifndef GA_SP_SELCAP
+#define GA_SP_SELCAP 4096
+#endif
+constexpr int kSelCap = GA_SP_SELCAP;                  // selected positions listed per window
 constexpr int kScanBlock = 1024;
 constexpr int kGapTable = 64;
 
@@ -246,7 +249,12 @@ struct FastDiv {
 //   [n, ld] element-major (ei = ld >= K, ek = 1): consecutive lanes read the K
 //     replicas of ONE element, i.e. one element's K=32 fp32 values are one
 //     128-B line -- the gather/write-back moves whole lines.
-constexpr int kGatherSlots = 2048;  // floats of LDS for the (element, replica) values
+#ifndef GA_SP_SLOTS
+#define GA_SP_SLOTS 2048
+#endif
+constexpr int kGatherSlots = GA_SP_SLOTS;  // floats of LDS for the (element, replica) values
+// (measured, K = 32 element-major: 2048 slots 0.075 ms, 4096 slots 0.090 ms -- the
+// 16 loads in flight per lane cost 95 VGPRs and occupancy; 3072: 0.097-0.107 ms)
 
 struct Rep {
     int64_t ek, ei;  // strides of replica and element

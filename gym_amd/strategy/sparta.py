@@ -19,10 +19,11 @@ mask_source=...)):
       parameter order (same generator calls, so the same selections and the
       same global RNG state afterwards), rank 0's masks broadcast as one uint8
       mask arena.  Bit-identical to the reference given the same generator.
-  "philox" (opt-in fast mode) — each element's Bernoulli(p) draw comes from
-      Philox4x32-10 keyed by a per-run seed (rank 0's torch.initial_seed(),
-      broadcast once) and the iteration; every rank computes the identical mask
-      in-kernel, so the per-step N-byte mask broadcast and the per-tensor
+  "philox" (opt-in fast mode) — each element is selected independently with
+      probability p, drawn in-kernel as the Geometric(p) gaps between selected
+      elements from Philox4x32-10 keyed by a per-run seed (rank 0's
+      torch.initial_seed(), broadcast once) and the iteration (include/gym_amd.h,
+      ga_sparta_gap_table); every rank computes the identical mask in-kernel, so the per-step N-byte mask broadcast and the per-tensor
       draws disappear.  Same distribution, a DIFFERENT random stream: selections
       are not the reference's, and the global torch RNG is not consumed.
       Tensors without a gradient are skipped as in the reference (a skip-range
