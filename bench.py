@@ -403,6 +403,43 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
             "ref_bytes_tx": plan.reference_bytes()}
 
 
+def bench_diloco_torch_gpu(args, coll, dev, fused_ms, model="gpt2-124m", K=8):
+    """The reference's DiLoCo outer step (diloco.py:34-76) as per-tensor torch
+    ops on this GPU, the un-fused baseline on the same hardware: for each of
+    the model's tensors the K nodes' values are summed and divided (the
+    all_reduce(SUM) + `/= num_nodes` of :34-37, here over K local replicas),
+    master.grad = master - avg (:43-45), torch.optim.SGD(lr 0.7, momentum
+    0.9, nesterov; foreach) steps the master (:70), and every node copies the
+    master (:47-49 + :39-41)."""
+    shapes = MODELS[model]()
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    base = [torch.randn(*sh, device=dev, generator=g) * 0.02 for sh in shapes]
+    reps = [[b + torch.randn(b.shape, device=dev, generator=g) * 1e-3 for b in base] for _ in range(K)]
+    master = [torch.nn.Parameter(b.clone()) for b in base]
+    opt = torch.optim.SGD(master, lr=0.7, momentum=0.9, nesterov=True)
+
+    @torch.no_grad()
+    def step():
+        for i, m in enumerate(master):
+            acc = reps[0][i].clone()
+            for k in range(1, K):
+                acc.add_(reps[k][i])
+            acc /= K
+            m.grad = m.data - acc
+        opt.step()
+        for i, m in enumerate(master):
+            for k in range(K):
+                reps[k][i].copy_(m.data)
+
+    t = timed_loop(step, max(3, args.steps // 4), 2, coll)
+    del reps, master, base
+    return {"ms_per_step": round(t * 1e3, 4), "model": model, "nodes": K, "tensors": len(shapes),
+            "fused_ms_per_step": round(fused_ms, 4), "fused_speedup": round(t * 1e3 / fused_ms, 2),
+            "what": "reference op sequence per tensor in torch on this GPU (sum over K replicas, divide, "
+                    "master grad, torch SGD-Nesterov foreach, copy to every node)"}
+
+
 def bench_inner_adamw(args, coll, dev, model="gpt2-124m", max_norm=1.0):
     """Inner optimizer step on one node's arena: fused
     clip + AdamW (ga_grad_clip_coef + ga_adam_step) vs torch.optim.AdamW
@@ -487,6 +524,9 @@ def main():
                 ("sparta_k32_rows", lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows")),
                 ("simple_reduce_char_k8", bench_simple),
                 ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
+        if coll.world == 1:
+            runs.insert(0, ("diloco_torch_per_tensor_gpu",
+                            lambda a, c, d: bench_diloco_torch_gpu(a, c, d, head["ms_per_step"])))
         if coll.world > 1:  # configs[2] as named: one node per GPU, the exchange alone over xGMI
             def diloco_1(a, c, d):
                 r = bench_diloco(argparse.Namespace(**{**vars(a), "replicas": 1}), c, d)
