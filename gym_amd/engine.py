@@ -27,6 +27,19 @@ def _f32(x):
 
 
 CHUNK_BYTES = 64 << 20  # pipeline chunk of the sharded exchange (RCCL stays at its large-message rate)
+# Below this arena size the exchange is latency-bound: ONE all-reduce (RCCL's
+# low-latency protocols, one launch) beats a reduce-scatter + shard kernel +
+# all-gather, and the replicated local update costs microseconds.
+SHARD_MIN_BYTES = 32 << 20
+
+
+def default_shard(coll, n, dtype):
+    """Shard the exchange (reduce-scatter -> shard kernel -> all-gather) when
+    the collective is RCCL across processes and the arena is large enough to
+    be bandwidth-bound; gloo (no reduce-scatter) and small arenas use one
+    all-reduce."""
+    esz = torch.empty((), dtype=dtype).element_size()
+    return bool(coll.rccl and coll.exchange and n * esz >= SHARD_MIN_BYTES)
 
 
 class ShardPlan:
@@ -123,7 +136,7 @@ class MeanReduce:
         self.coll, self.K_local, self.n = coll, int(K_local), int(n)
         self.K_total = coll.world * self.K_local
         W, X = coll.world, coll.exchange
-        self.shard = (coll.rccl and X) if shard is None else (shard and X)
+        self.shard = default_shard(coll, self.n, dtype) if shard is None else bool(shard and X)
         if self.shard:
             esz = torch.empty((), dtype=dtype).element_size()
             self.plan = ShardPlan(self.n, W, coll.rank, esz, chunks)
@@ -164,8 +177,8 @@ class DiLoCoOuter:
         self.K_total = coll.world * self.K_local
         self.hp = dict(lr=lr, momentum=momentum, nesterov=nesterov, dampening=dampening, weight_decay=weight_decay)
         W, X = coll.world, coll.exchange
-        self.shard = (coll.rccl and X) if shard is None else (shard and X)
         self.n = int(n)
+        self.shard = default_shard(coll, self.n, dtype) if shard is None else bool(shard and X)
         if self.shard:
             esz = torch.empty((), dtype=dtype).element_size()
             self.plan = ShardPlan(self.n, W, coll.rank, esz, chunks)

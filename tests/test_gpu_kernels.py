@@ -335,6 +335,39 @@ def test_sparta_select_scatter_element_major_padded_rows():
     assert (got[:, K:] == 5.0).all()
 
 
+@pytest.mark.parametrize("src,p", [("philox", 1.0), ("philox", 0.9), ("philox", 0.0), ("mask", 0.95)])
+def test_sparta_dense_selection_windows(src, p):
+    """Selections denser than one list window per 16384-element tile (kSelCap):
+    p = 1 (every element: 17 Philox calls per 64-element group), p = 0.9, a
+    95%-dense uint8 mask; p = 0 selects nothing.  List and fused forms."""
+    from gym_amd import ops
+    n, K = 70_001, 2
+    rng = np.random.default_rng(int(p * 100))
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    seed, it = 5, 11
+    mask_t = None
+    if src == "mask":
+        m = rng.random(n) < p
+        mask_t = torch.zeros(n + 15, dtype=torch.uint8, device=DEV)
+        mask_t[:n] = torch.from_numpy(m.astype(np.uint8)).to(DEV)
+    else:
+        m = osparta.philox_mask(n, seed, it, p)
+    cap = int(m.sum()) + 16
+    idx, count, work = _sparta_buffers(n, cap)
+    vals = torch.empty(cap, device=DEV)
+    a = t(x)
+    ops.sparta_select(a, n, cap, idx, vals, count, work, mask=mask_t, seed=seed, iteration=it, p=p)
+    c = int(count[0].item())
+    assert c == int(m.sum()) and np.array_equal(idx[:c].cpu().numpy(), np.flatnonzero(m))
+    assert np.array_equal(host(vals)[:c], oreduce.mean_reduce(list(x[:, m]), divisor=1))
+    b = t(x)
+    ops.sparta_average_local(b, n, float(K), mask=mask_t, seed=seed, iteration=it, p=p)
+    want = osparta.sparse_average(list(x), m)
+    got = host(b)
+    for k in range(K):
+        assert np.array_equal(got[k], want[k])
+
+
 def test_sparta_overflow_flag():
     from gym_amd import ops
     n = 10_000

@@ -63,3 +63,21 @@ def test_replica_processes_use_rccl(stub):
 def test_cpu_devices_are_refused(stub, device):
     with pytest.raises(ValueError, match="Invalid device"):
         _trainer(rank=0, num_nodes=2, device=device)._build_connection()
+
+
+def test_exchange_sharding_follows_arena_size():
+    """RCCL across processes: arenas of >= 32 MB take the reduce-scatter ->
+    shard kernel -> all-gather pipeline (bandwidth-bound, outer state / world),
+    smaller ones one all-reduce (latency-bound, e.g. the char-level model of
+    configs[1]: 3.7 MB); gloo and world size 1 never shard."""
+    from types import SimpleNamespace
+
+    from gym_amd.engine import SHARD_MIN_BYTES, default_shard
+    from gym_amd.shapes import MODELS, numel
+    rccl8 = SimpleNamespace(rccl=True, exchange=True)
+    assert default_shard(rccl8, numel(MODELS["gpt2-124m"]()), torch.float32)
+    assert not default_shard(rccl8, numel(MODELS["gpt2-char"]()), torch.float32)
+    assert default_shard(rccl8, SHARD_MIN_BYTES // 4, torch.float32)
+    assert not default_shard(rccl8, SHARD_MIN_BYTES // 4, torch.bfloat16)
+    assert not default_shard(SimpleNamespace(rccl=False, exchange=True), 1 << 30, torch.float32)
+    assert not default_shard(SimpleNamespace(rccl=True, exchange=False), 1 << 30, torch.float32)
