@@ -58,6 +58,10 @@ def _synth(shapes, rank, seed=1234):
 
 
 def _time_worker(rank, world, port, shapes, threads, steps, warmup, out_path):
+    # gloo prints its connection banner on stdout: keep the parent's stdout (the
+    # bench's one JSON line) clean
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(devnull, 1)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(threads)
