@@ -266,7 +266,11 @@ struct Rep {
 // (ga_sparta_average_local): each selected element's average is written back
 // to every replica right after its gather, while its lines are still in L2
 // (full-line write-backs instead of partial writes from a later scatter pass).
-template <typename T>
+// V4: element-major set whose rows are 4-replica aligned (K % 4 == 0, ld % 4 == 0,
+// base aligned to 4 elements): each lane moves one 4-replica vector, so an element's
+// K = 32 fp32 replicas are 8 lanes x 16 B and the gather issues a quarter of the
+// loads and address computations.
+template <typename T, bool V4>
 __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t n, const int32_t* tile_offsets,
                                                                  T* src, int64_t K, Rep R,
                                                                  int64_t cap, int32_t* __restrict__ idx,
@@ -311,7 +315,55 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
         const int wtot = (total - w0) < kSelCap ? (total - w0) : kSelCap;
         for (int c0 = 0; c0 < wtot; c0 += per_pass) {
             const int ce = (wtot - c0) < per_pass ? (wtot - c0) : per_pass;
-            if (K <= kGatherSlots) {
+            if (V4) {
+                // lane f -> (element e, replica quad q); staged into LDS per element at
+                // the odd stride Kp, summed in ascending replica order as below
+                using V = typename Vec4<T>::type;
+                const int Kq = Ki >> 2;
+                const FastDiv divQ((uint32_t)Kq);
+                constexpr int kLoads4 = kGatherSlots / 4 / kSpBlock;
+                const int nf = ce * Kq;
+                float v[kLoads4][4];
+#pragma unroll
+                for (int u = 0; u < kLoads4; ++u) {
+                    const int f = threadIdx.x + u * kSpBlock;
+                    if (f < nf) {
+                        const int e = (int)divQ.div(f), q = f - e * Kq;
+                        Vec4<T>::unpack(*reinterpret_cast<const V*>(src + R.at(tile0 + sel_list[c0 + e], 4 * q)), v[u]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kLoads4; ++u) {
+                    const int f = threadIdx.x + u * kSpBlock;
+                    if (f < nf) {
+                        const int e = (int)divQ.div(f), q = f - e * Kq;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) gv[e * Kp + 4 * q + r] = v[u][r];
+                    }
+                }
+                __syncthreads();
+                if (threadIdx.x < ce) {
+                    float acc = 0.f;
+                    for (int k = 0; k < Ki; ++k) acc += gv[threadIdx.x * Kp + k];
+                    const int64_t pos = out0 + w0 + c0 + threadIdx.x;
+                    if (vals && pos < cap) Elem<T>::store(vals + pos, acc);
+                    if (divisor > 0.f) gavg[threadIdx.x] = acc / divisor;
+                }
+                __syncthreads();
+                if (divisor > 0.f) {
+#pragma unroll
+                    for (int u = 0; u < kLoads4; ++u) {
+                        const int f = threadIdx.x + u * kSpBlock;
+                        if (f < nf) {
+                            const int e = (int)divQ.div(f), q = f - e * Kq;
+                            const float a = gavg[e];
+                            const float w[4] = {a, a, a, a};
+                            *reinterpret_cast<V*>(src + R.at(tile0 + sel_list[c0 + e], 4 * q)) = Vec4<T>::pack(w);
+                        }
+                    }
+                    __syncthreads();
+                }
+            } else if (K <= kGatherSlots) {
                 // lane f -> (element e, replica k): replica-major for [K, ld] rows,
                 // element-major for [n, ld] (one element's replicas on adjacent lanes)
                 // every lane's loads of the pass issued back to back (one HBM latency
@@ -421,8 +473,14 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
                            tile_offsets, cap, count);
         if (int e = check_launch("ga_sparta_select(scan)")) return e;
     }
-    hipLaunchKernelGGL((sparta_select_kernel<T>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
-                       tile_offsets, (T*)src, K, R, cap, idx, (T*)vals, divisor);
+    const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlots && R.ei % 4 == 0 &&
+                    ((uintptr_t)src % (4 * sizeof(T))) == 0;
+    if (v4)
+        hipLaunchKernelGGL((sparta_select_kernel<T, true>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
+                           tile_offsets, (T*)src, K, R, cap, idx, (T*)vals, divisor);
+    else
+        hipLaunchKernelGGL((sparta_select_kernel<T, false>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
+                           tile_offsets, (T*)src, K, R, cap, idx, (T*)vals, divisor);
     return check_launch("ga_sparta_select(gather)");
 }
 

@@ -662,6 +662,33 @@ def test_sparta_bf16_and_many_replicas():
             np.testing.assert_allclose(got[k], want[k], rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("K,dtype,ld", [(8, torch.bfloat16, 8), (32, torch.bfloat16, 32), (12, torch.float32, 16),
+                                         (12, torch.float32, 14)])
+def test_sparta_element_major_vector_rows(K, dtype, ld):
+    """Element-major sets whose rows take 4-replica vector loads (K and the row
+    stride multiples of 4; bf16 and fp32) and one whose stride (14) does not:
+    the same selections and ascending-replica means either way."""
+    from gym_amd import ops
+    n, p = 150_001, 0.02
+    x = np.random.default_rng(K + ld).standard_normal((K, n)).astype(np.float32)
+    buf = torch.full((n, ld), 7.0, device=DEV, dtype=dtype)
+    buf[:, :K] = t(np.ascontiguousarray(x.T), dtype)
+    xs = buf[:, :K].float().cpu().numpy().T
+    m = osparta.philox_mask(n, 21, 4, p)
+    cap = int(m.sum()) + 8
+    idx, count, work = _sparta_buffers(n, cap)
+    vals = torch.empty(cap, device=DEV, dtype=dtype)
+    ops.sparta_average_local(buf[:, :K], n, float(K), seed=21, iteration=4, p=p, idx=idx, vals=vals, cap=cap,
+                             count=count, work=work, layout="elem")
+    c = int(count[0].item())
+    assert c == int(m.sum()) and np.array_equal(idx[:c].cpu().numpy(), np.flatnonzero(m))
+    want = osparta.sparse_average(list(xs), m)
+    got = buf.float().cpu().numpy()
+    tol = 1e-2 if dtype == torch.bfloat16 else 0
+    np.testing.assert_allclose(got[:, :K].T, np.stack(want), rtol=tol, atol=tol)
+    assert (got[:, K:] == 7.0).all()
+
+
 def test_replica_mean_edge_sizes():
     from gym_amd import ops
     empty = torch.zeros(0, device=DEV)
