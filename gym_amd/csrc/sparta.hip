@@ -252,7 +252,12 @@ struct FastDiv {
 #ifndef GA_SP_SLOTS
 #define GA_SP_SLOTS 2048
 #endif
+#ifndef GA_SP_SLOTS_V4
+#define GA_SP_SLOTS_V4 3072
+#endif
 constexpr int kGatherSlots = GA_SP_SLOTS;  // floats of LDS for the (element, replica) values
+constexpr int kGatherSlotsV4 = GA_SP_SLOTS_V4;  // the same for the 4-replica vector form
+// (measured, K = 32: 2048 slots 0.058-0.060 ms, 3072 0.053-0.056 ms, 4096 0.055-0.056 ms)
 // (measured, K = 32 element-major: 2048 slots 0.075 ms, 4096 slots 0.090 ms -- the
 // 16 loads in flight per lane cost 95 VGPRs and occupancy; 3072: 0.097-0.107 ms)
 
@@ -278,7 +283,8 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
     __shared__ int wave_tot[4];
     __shared__ uint64_t tab[kGapTable];
     __shared__ uint16_t sel_list[kSelCap];  // tile-local positions (< 16384) of one window
-    __shared__ float gv[kGatherSlots];
+    constexpr int kSlots = V4 ? kGatherSlotsV4 : kGatherSlots;
+    __shared__ float gv[kSlots];
     __shared__ float gavg[kSpBlock];
     load_gap_table(P, tab);
     const int64_t tile0 = (int64_t)blockIdx.x * kSpTile;
@@ -291,9 +297,9 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
     // entry's K values sit at an odd LDS stride Kp (K, or K + 1 for even K), so
     // lanes of consecutive entries (the rows layout's stores, every layout's
     // per-entry sums) hit distinct banks instead of one bank at K = 32.
-    const int Ki = (int)(K < kGatherSlots ? K : kGatherSlots);
-    const int Kp = (Ki & 1) || Ki + 1 > kGatherSlots ? Ki : Ki + 1;
-    const int per_pass = K >= kGatherSlots ? 1 : (kGatherSlots / Kp < kSpBlock ? kGatherSlots / Kp : kSpBlock);
+    const int Ki = (int)(K < kSlots ? K : kSlots);
+    const int Kp = (Ki & 1) || Ki + 1 > kSlots ? Ki : Ki + 1;
+    const int per_pass = K >= kSlots ? 1 : (kSlots / Kp < kSpBlock ? kSlots / Kp : kSpBlock);
     const FastDiv divK((uint32_t)Ki);
     // the tile's selected elements in windows of kSelCap list slots (one window
     // unless p is large)
@@ -315,13 +321,13 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
         const int wtot = (total - w0) < kSelCap ? (total - w0) : kSelCap;
         for (int c0 = 0; c0 < wtot; c0 += per_pass) {
             const int ce = (wtot - c0) < per_pass ? (wtot - c0) : per_pass;
-            if (V4) {
+            if constexpr (V4) {
                 // lane f -> (element e, replica quad q); staged into LDS per element at
                 // the odd stride Kp, summed in ascending replica order as below
                 using V = typename Vec4<T>::type;
                 const int Kq = Ki >> 2;
                 const FastDiv divQ((uint32_t)Kq);
-                constexpr int kLoads4 = kGatherSlots / 4 / kSpBlock;
+                constexpr int kLoads4 = kSlots / 4 / kSpBlock;
                 const int nf = ce * Kq;
                 float v[kLoads4][4];
 #pragma unroll
@@ -363,7 +369,8 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
                     }
                     __syncthreads();
                 }
-            } else if (K <= kGatherSlots) {
+            } else {
+            if (K <= kSlots) {
                 // lane f -> (element e, replica k): replica-major for [K, ld] rows,
                 // element-major for [n, ld] (one element's replicas on adjacent lanes)
                 // every lane's loads of the pass issued back to back (one HBM latency
@@ -417,6 +424,7 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
                     const float a = acc / divisor;
                     for (int64_t k = 0; k < K; ++k) Elem<T>::store(src + R.at(i, k), a);
                 }
+            }
             }
         }
         __syncthreads();
@@ -473,7 +481,7 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
                            tile_offsets, cap, count);
         if (int e = check_launch("ga_sparta_select(scan)")) return e;
     }
-    const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlots && R.ei % 4 == 0 &&
+    const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlotsV4 && R.ei % 4 == 0 &&
                     ((uintptr_t)src % (4 * sizeof(T))) == 0;
     if (v4)
         hipLaunchKernelGGL((sparta_select_kernel<T, true>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
