@@ -434,8 +434,9 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
 // Scatter: one lane per (element, replica) pair, so every lane stores.
 // [K, ld] rows: replicas on the grid's y dimension (no per-lane division);
 // element-major: consecutive lanes store the K replicas of one element (one
-// line per element at K = 32 fp32).
-template <typename T>
+// line per element at K = 32 fp32), as 4-replica vectors (V4) when the rows
+// are 4-aligned; pair indices in 32-bit arithmetic when cap * K < 2^31 (W32).
+template <typename T, bool V4, bool W32>
 __global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __restrict__ vals,
                                                                   const int32_t* __restrict__ idx,
                                                                   const int64_t* __restrict__ count, int64_t cap,
@@ -443,9 +444,24 @@ __global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __res
     const int64_t m = count[0] < cap ? count[0] : cap;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     if (R.em) {
-        for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m * K; t += stride) {
-            const int64_t j = t / K, k = t - j * K;
-            Elem<T>::store(dst + R.at(idx[j], k), Elem<T>::load(vals + j) / divisor);
+        const int64_t Kv = V4 ? K / 4 : K;  // lanes per element
+        const int64_t tot = m * Kv;
+        for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += stride) {
+            int64_t j, q;
+            if (W32) {
+                j = (int64_t)((uint32_t)t / (uint32_t)Kv);
+                q = t - j * Kv;
+            } else {
+                j = t / Kv;
+                q = t - j * Kv;
+            }
+            const float a = Elem<T>::load(vals + j) / divisor;
+            if (V4) {
+                const float w[4] = {a, a, a, a};
+                *reinterpret_cast<typename Vec4<T>::type*>(dst + R.at(idx[j], 4 * q)) = Vec4<T>::pack(w);
+            } else {
+                Elem<T>::store(dst + R.at(idx[j], q), a);
+            }
         }
         return;
     }
@@ -453,6 +469,24 @@ __global__ __launch_bounds__(kSpBlock) void sparta_scatter_kernel(const T* __res
         T* d = dst + k * R.ek;
         for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride)
             Elem<T>::store(d + idx[j], Elem<T>::load(vals + j) / divisor);
+    }
+}
+
+template <typename T>
+static void launch_scatter(dim3 grid, hipStream_t stream, const void* vals, const int32_t* idx,
+                           const int64_t* count, int64_t cap, float divisor, void* dst, int64_t K, Rep R) {
+    const bool v4 = R.em && K % 4 == 0 && R.ei % 4 == 0 && ((uintptr_t)dst % (4 * sizeof(T))) == 0;
+    const bool w32 = cap * K < ((int64_t)1 << 31);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(kSpBlock), 0, stream, (const T*)vals, idx, count, cap, divisor, (T*)dst,
+                           K, R);
+    };
+    if (v4) {
+        if (w32) go(sparta_scatter_kernel<T, true, true>);
+        else go(sparta_scatter_kernel<T, true, false>);
+    } else {
+        if (w32) go(sparta_scatter_kernel<T, false, true>);
+        else go(sparta_scatter_kernel<T, false, false>);
     }
 }
 
@@ -597,14 +631,8 @@ extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32
     const dim3 grid = R.em ? dim3((unsigned)stream_grid(cap * K, kSpBlock)) :
                              dim3(gx > 64 ? 64 : gx, (unsigned)(K < 65535 ? K : 65535));
     switch (dtype) {
-        case GA_F32:
-            hipLaunchKernelGGL((sparta_scatter_kernel<float>), grid, dim3(kSpBlock), 0, stream,
-                               (const float*)vals, idx, count, cap, divisor, (float*)dst, K, R);
-            break;
-        case GA_BF16:
-            hipLaunchKernelGGL((sparta_scatter_kernel<__hip_bfloat16>), grid, dim3(kSpBlock), 0, stream,
-                               (const __hip_bfloat16*)vals, idx, count, cap, divisor, (__hip_bfloat16*)dst, K, R);
-            break;
+        case GA_F32: launch_scatter<float>(grid, stream, vals, idx, count, cap, divisor, dst, K, R); break;
+        case GA_BF16: launch_scatter<__hip_bfloat16>(grid, stream, vals, idx, count, cap, divisor, dst, K, R); break;
         default: set_error("ga_sparta_scatter: unknown dtype %d", dtype); return GA_EINVAL;
     }
     return check_launch("ga_sparta_scatter");

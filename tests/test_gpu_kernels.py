@@ -687,6 +687,14 @@ def test_sparta_element_major_vector_rows(K, dtype, ld):
     tol = 1e-2 if dtype == torch.bfloat16 else 0
     np.testing.assert_allclose(got[:, :K].T, np.stack(want), rtol=tol, atol=tol)
     assert (got[:, K:] == 7.0).all()
+    # the multi-rank form: select + gather into the packed list, scatter back
+    buf2 = torch.full((n, ld), 7.0, device=DEV, dtype=dtype)
+    buf2[:, :K] = t(np.ascontiguousarray(x.T), dtype)
+    ops.sparta_select(buf2[:, :K], n, cap, idx, vals, count, work, seed=21, iteration=4, p=p, layout="elem")
+    ops.sparta_scatter(vals, idx, count, cap, float(K), buf2[:, :K], layout="elem")
+    got2 = buf2.float().cpu().numpy()
+    np.testing.assert_allclose(got2[:, :K].T, np.stack(want), rtol=tol, atol=tol)
+    assert (got2[:, K:] == 7.0).all()
 
 
 def test_replica_mean_edge_sizes():
