@@ -14,6 +14,7 @@ inputs:
   demo_codec.npz    G4  _dct/_idct bases, _get_smaller_split, TransformDCT encode/decode,
                         CompressDCT compress/decompress/batch_decompress (demo_impl/demo.py)
   demo_steps.npz    G4  3 full DeMo.step()s with K=2 over gloo (demo.py:142-209)
+  demo_steps_bf16.npz G4b the same on bf16 parameters (bf16 bases, demo.py:235-236)
   lr_schedule.npz   G5  lambda_cosine LR sequence (strategy.py:65-95)
 """
 import os
@@ -334,21 +335,60 @@ def g4_step_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def gen_g4_steps():
-    K = 2
-    out = run_spawn(g4_step_worker, K)
-    res = {"K": K, "steps": DEMO_STEPS, "nshapes": len(DEMO_STEP_SHAPES), "lr": 0.01, "wd": 0.1,
-           "decay": 0.999, "topk": 32, "chunk": 64}
+def _gen_demo_steps(worker, shapes, fname, K=2, **extra):
+    out = run_spawn(worker, K)
+    res = {"K": K, "steps": DEMO_STEPS, "nshapes": len(shapes), "lr": 0.01, "wd": 0.1,
+           "decay": 0.999, "topk": 32, "chunk": 64, **extra}
     for step in range(DEMO_STEPS):
         res[f"tx_{step}"] = out[0][f"tx_{step}"]
         res[f"rx_{step}"] = out[0][f"rx_{step}"]
-        for i in range(len(DEMO_STEP_SHAPES)):
+        for i in range(len(shapes)):
             for key in ("grad", "delta_before", "delta_after"):
                 res[f"{key}_{step}_{i}"] = np.stack([out[r][f"{key}_{step}"][i] for r in range(K)])
             for key in ("p_before", "p_after", "sign"):
                 res[f"{key}_{step}_{i}"] = out[0][f"{key}_{step}"][i]
                 assert np.array_equal(out[1][f"{key}_{step}"][i], out[0][f"{key}_{step}"][i])
-    np.savez_compressed(os.path.join(OUT, "demo_steps.npz"), **res)
+    np.savez_compressed(os.path.join(OUT, fname), **res)
+
+
+def gen_g4_steps():
+    _gen_demo_steps(g4_step_worker, DEMO_STEP_SHAPES, "demo_steps.npz")
+
+
+# bf16 parameters: the reference casts its DCT bases to p.dtype (demo.py:235-236), so
+# every einsum, the top-k and the scatter-mean run in bf16 on the CPU.  Values are
+# stored as their exact fp32 widening (npz has no bf16).
+DEMO_BF16_SHAPES = [(128, 128), (128, 64), (768,), (64,)]
+
+
+def g4_bf16_worker(rank, world, port, q):
+    from exogym.strategy.demo_impl.demo import DeMo
+    from exogym.strategy.communicate import all_gather
+    init(rank, world, port)
+    model = ShapeModel(DEMO_BF16_SHAPES, seed=8765).to(torch.bfloat16)
+    opt = DeMo(model.parameters(), compression_decay=0.999, compression_topk=32, compression_chunk=64,
+               weight_decay=0.1, custom_all_gather=all_gather, lr=0.01)
+    rec = {}
+    f = lambda t: t.detach().float().numpy().copy()  # noqa: E731
+    for step in range(DEMO_STEPS):
+        g = torch.Generator().manual_seed(3000 + 10 * rank + step)
+        for p in model.parameters():
+            p.grad = torch.randn(p.shape, generator=g).to(torch.bfloat16)
+        rec[f"grad_{step}"] = [f(p.grad) for p in model.parameters()]
+        rec[f"p_before_{step}"] = [f(p) for p in model.parameters()]
+        rec[f"delta_before_{step}"] = [f(opt.demo_state[p]["delta"]) for p in model.parameters()]
+        opt.step()
+        rec[f"p_after_{step}"] = [f(p) for p in model.parameters()]
+        rec[f"delta_after_{step}"] = [f(opt.demo_state[p]["delta"]) for p in model.parameters()]
+        rec[f"sign_{step}"] = [f(p.grad) for p in model.parameters()]
+        rec[f"tx_{step}"] = opt.data_transmit
+        rec[f"rx_{step}"] = opt.data_receive
+    q.put((rank, rec))
+    dist.destroy_process_group()
+
+
+def gen_g4_bf16():
+    _gen_demo_steps(g4_bf16_worker, DEMO_BF16_SHAPES, "demo_steps_bf16.npz", dtype="bfloat16")
 
 
 # ---------------------------------------------------------------- G5 --------
@@ -385,8 +425,8 @@ def gen_g5():
 
 if __name__ == "__main__":
     torch.set_num_threads(1)
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4c", "g4s", "g5"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4c", "g4s", "g4b", "g5"]
     for w in which:
         {"g1": gen_g1, "g2": gen_g2, "g3": gen_g3, "g3b": gen_g3b, "g4c": gen_g4_codec,
-         "g4s": gen_g4_steps, "g5": gen_g5}[w]()
+         "g4s": gen_g4_steps, "g4b": gen_g4_bf16, "g5": gen_g5}[w]()
         print("wrote", w, flush=True)

@@ -550,6 +550,47 @@ def test_demo_matches_reference_golden_steps(golden):
     tally.done()
 
 
+def test_demo_bf16_vs_reference_bf16_golden(golden):
+    """Three DeMo.step()s of the reference on bf16 parameters (K=2 over gloo,
+    tests/golden/demo_steps_bf16.npz) replayed as 2 replicas.  The reference runs
+    its DCT in bf16 (bases cast to bf16, every einsum stage rounded) and breaks the
+    many bf16 top-k ties in torch's CPU selection order, so bit-parity is not
+    defined for bf16; the bars are the statistical ones of
+    demo_checks.bf16_agreement, which the fp64 oracle also meets on the same
+    inputs (test_oracle_golden.py::test_oracle_vs_reference_bf16_golden)."""
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    z = golden("demo_steps_bf16.npz")
+    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
+    lr, wd, decay = float(z["lr"]), float(z["wd"]), float(z["decay"])
+    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
+    L = ArenaLayout(shapes)
+    plan = DemoPlan(L, chunk=int(z["chunk"]), topk=int(z["topk"]))
+    assert plan.reference_bytes(2) == int(z["tx_0"])
+    P, D, G = (torch.zeros(K, L.n, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    payload = torch.zeros(K, 2 * plan.M, dtype=torch.int32, device=DEV)
+    wdf = float(np.float32(1.0 - lr * wd))
+    agree = demo_checks.Bf16Agreement()
+    for step in range(steps):
+        for i in range(ns):
+            for k in range(K):
+                L.views(P[k])[i].copy_(t(z[f"p_before_{step}_{i}"], torch.bfloat16))
+                L.views(D[k])[i].copy_(t(z[f"delta_before_{step}_{i}"][k], torch.bfloat16))
+                L.views(G[k])[i].copy_(t(z[f"grad_{step}_{i}"][k], torch.bfloat16))
+        P0 = P.clone()
+        ops.demo_encode(plan, P, G, D, payload, lr, decay, wdf)
+        ops.demo_decode(plan, payload, P, G, lr)
+        # the reference's own update ops (demo.py:159-160, torch SGD p.add_(grad, alpha=-lr)) as torch
+        # runs them on this GPU in bf16, fed our signs: bit-identical to the kernel's update
+        want = P0.mul_(1.0 - lr * wd).add_(G, alpha=-lr)
+        assert torch.equal(want, P), "bf16 p update differs from torch's bf16 mul_/add_ on the GPU"
+        for i in range(ns):
+            agree.check(host(L.views(G[0])[i]), host(L.views(P[0])[i]), [host(L.views(D[k])[i]) for k in range(K)],
+                        z, step, i)
+    agree.done()
+
+
 @pytest.mark.parametrize("kernel", ["wave", "block"])
 def test_demo_all_zero_chunk_tie_rule(monkeypatch, kernel):
     from gym_amd import ops

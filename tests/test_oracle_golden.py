@@ -258,6 +258,30 @@ def test_demo_full_steps_match_reference(golden):
                 close(deltas[r], ref_d, rtol=0, atol=1e-5 * scale)
 
 
+def test_oracle_vs_reference_bf16_golden(golden):
+    """G4b: the reference's DeMo on bf16 parameters.  The oracle computes in fp64
+    from the bf16 values and rounds the stored p / delta to bf16 as the kernels
+    do; the bf16 bar is statistical (demo_checks.Bf16Agreement)."""
+    import demo_checks
+    z = golden("demo_steps_bf16.npz")
+    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
+    lr, wd, decay = float(z["lr"]), float(z["wd"]), float(z["decay"])
+    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
+    assert odemo.transmit_bytes(shapes, 64, 32, val_itemsize=2) == int(z["tx_0"])
+    rb = demo_checks.bf16_round
+    agree = demo_checks.Bf16Agreement()
+    for step in range(steps):
+        for i in range(ns):
+            p0 = z[f"p_before_{step}_{i}"]
+            _, deltas, sgn, _ = odemo.demo_step(p0, list(z[f"delta_before_{step}_{i}"]),
+                                                list(z[f"grad_{step}_{i}"]), lr, decay, 32, 64, wd)
+            p_wd = rb(p0 * np.float32(1.0 - lr * wd))
+            p_new = rb(p_wd - np.float32(lr) * sgn.astype(np.float32))
+            agree.check(sgn, p_new, [rb(d) for d in deltas], z, step, i)
+    frac, worst = agree.done()
+    assert worst < 1.0  # the bf16 ties do show up: the check is not vacuous
+
+
 # ---- G5 schedule ------------------------------------------------------------
 def test_lambda_cosine_matches_reference(golden):
     z = golden("lr_schedule.npz")
