@@ -431,6 +431,149 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
     }
 }
 
+// Single-process average without the packed list (ga_sparta_average_local with
+// no idx/vals/count) on an element-major set with 4-aligned rows and K = 4*KQ
+// replicas, KQ | 64: one WAVEFRONT per 4096-element tile, waves synchronised
+// only with themselves (no workgroup barrier after the gap table), so a SIMD
+// mixes waves drawing their mask with waves whose gathers are in flight.  The
+// wave scans its lanes' selection counts with shuffles, lists the selected
+// positions in its own LDS, then moves each element's K values as KQ lanes x
+// one 4-replica vector (whole 128-B lines at K = 32 fp32), up to 4 passes of
+// loads in flight per lane, stages them at an odd LDS stride, sums each element
+// in ascending replica order and divides (the tile-gather kernel's fp32 order:
+// bit-identical), and writes the average back to every replica.
+// Measured (K = 32, 124M, p = 0.005): 0.049-0.053 ms against 0.054-0.063 ms for
+// the 16384-element tile-gather kernel; a persistent form that draws tile t+1's
+// mask while tile t's loads are in flight ran 0.062 / 0.065 / 0.074 ms at 2 / 4 /
+// 8 tiles per wave (fewer waves in flight), and splitting the kernel's work
+// measured mask only 0.015 ms, gather only 0.034 ms.
+constexpr int kWTile = 64 * kSpPerThread;  // elements per wavefront tile
+constexpr int kWList = 256;                // listed positions per window
+#ifndef GA_SP_WAVES
+#define GA_SP_WAVES 4  // wavefronts (independent tiles) per workgroup
+#endif
+#ifndef GA_SP_EXPERIMENT
+#define GA_SP_EXPERIMENT 0  // timing experiments (tools/ab_sparta_wave.sh): 1 mask only, 2 gather only
+#endif
+
+// orders this wave's LDS accesses (the wave is the only writer of its slices)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One batch (<= EB listed elements from list[b0]): loads, LDS staging, ascending
+// replica sums, divide, write-back.
+template <typename T, int KQ>
+struct WaveBatch {
+    static constexpr int K = 4 * KQ, Kp = K + 1, EPP = 64 / KQ, EB = 4 * EPP;
+    using V = typename Vec4<T>::type;
+    __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0, int ne,
+                                               int lane, float* stage, float divisor) {
+        const int q = lane % KQ, el = lane / KQ;
+        V v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = u * EPP + el;
+            if (e < ne) v[u] = *reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = u * EPP + el;
+            if (e < ne) {
+                float f[4];
+                Vec4<T>::unpack(v[u], f);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) stage[e * Kp + 4 * q + r] = f[r];
+            }
+        }
+        wave_sync();
+        for (int e = lane; e < ne; e += 64) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc += stage[e * Kp + k];
+            stage[e * Kp] = acc / divisor;
+        }
+        wave_sync();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = u * EPP + el;
+            if (e < ne) {
+                const float a = stage[e * Kp];
+                const float w[4] = {a, a, a, a};
+                *reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q) = Vec4<T>::pack(w);
+            }
+        }
+        wave_sync();
+    }
+};
+
+template <typename T, int KQ>
+__global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(Pred P, int64_t n, T* __restrict__ src,
+                                                                               int64_t ld, float divisor) {
+    using B = WaveBatch<T, KQ>;
+    __shared__ uint64_t tab[kGapTable];
+    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
+    __shared__ float stages[GA_SP_WAVES][B::EB * B::Kp];
+    load_gap_table(P, tab);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint16_t* list = lists[wid];
+    float* stage = stages[wid];
+    const int64_t t = (int64_t)blockIdx.x * GA_SP_WAVES + wid;
+    const int64_t tile0 = t * kWTile;
+    const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
+#if GA_SP_EXPERIMENT == 2  // no mask: a fixed ~20-per-wave pattern (timing experiment only)
+    const uint64_t bits = (e0 < n && lane % 3 == 0) ? 1ull << (t % 64) : 0ull;
+#else
+    const uint64_t bits = e0 < n ? pred_bits64(P, tab, e0, n) : 0ull;
+#endif
+#if GA_SP_EXPERIMENT == 1  // mask only, no gather (timing experiment only)
+    if (__popcll(bits) == 1000) src[0] = (T)0.f;
+    return;
+#endif
+    const int c = __popcll(bits);
+    int x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    const int total = __shfl(x, 63, 64);
+    const int local0 = x - c;
+    for (int w0 = 0; w0 < total; w0 += kWList) {  // one window unless p is large
+        {
+            uint64_t b = bits;
+            int l = local0;
+            while (b) {
+                const int j = __builtin_ctzll(b);
+                b &= b - 1;
+                if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * kSpPerThread + j);
+                ++l;
+            }
+        }
+        wave_sync();
+        const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
+        for (int b0 = 0; b0 < wtot; b0 += B::EB)
+            B::run(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, stage, divisor);
+    }
+}
+
+template <typename T>
+static bool launch_average_wave(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
+                                float divisor) {
+    const dim3 grid((unsigned)ceil_div(ceil_div(n, kWTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, (T*)src, ld, divisor); };
+    switch (K) {
+        case 4: go(sparta_average_wave_kernel<T, 1>); return true;
+        case 8: go(sparta_average_wave_kernel<T, 2>); return true;
+        case 16: go(sparta_average_wave_kernel<T, 4>); return true;
+        case 32: go(sparta_average_wave_kernel<T, 8>); return true;
+        case 64: go(sparta_average_wave_kernel<T, 16>); return true;
+        default: return false;
+    }
+}
+
 // Scatter: one lane per (element, replica) pair, so every lane stores.
 // [K, ld] rows: replicas on the grid's y dimension (no per-lane division);
 // element-major: consecutive lanes store the K replicas of one element (one
@@ -517,6 +660,9 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
     }
     const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlotsV4 && R.ei % 4 == 0 &&
                     ((uintptr_t)src % (4 * sizeof(T))) == 0;
+    if (v4 && !tile_offsets && !vals && divisor > 0.f && launch_average_wave<T>(stream, P, n, (void*)src, R.ei, K,
+                                                                                divisor))
+        return check_launch("ga_sparta_average_local(wave)");
     if (v4)
         hipLaunchKernelGGL((sparta_select_kernel<T, true>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
                            tile_offsets, (T*)src, K, R, cap, idx, (T*)vals, divisor);

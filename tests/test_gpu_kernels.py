@@ -797,3 +797,39 @@ def test_demo_decode_sources_with_collisions(monkeypatch, S, kernel):
             np.testing.assert_allclose(gP[k, off:off + nel].reshape(shape), p0 - lr * s, rtol=0, atol=1e-7)
     for o, nel, o2 in zip(L.offsets, L.numels, L.offsets[1:] + [L.n]):  # padding untouched
         assert (gS[:, o + nel:o2] == 7.0).all()
+
+
+@pytest.mark.parametrize("K,dtype,ld,p", [(32, torch.float32, 32, 0.005), (32, torch.float32, 36, 0.3),
+                                          (4, torch.float32, 4, 1.0), (64, torch.float32, 64, 0.02),
+                                          (68, torch.float32, 68, 0.02), (32, torch.bfloat16, 32, 0.05),
+                                          (8, torch.bfloat16, 12, 0.5)])
+def test_sparta_average_local_own_groups(K, dtype, ld, p):
+    """ga_sparta_average_local without the packed list on a 4-aligned element-major
+    set (each lane averages its own 64-element group's selections in registers,
+    K <= 64; K = 68 takes the tile-gather kernel): the Philox selection with skip
+    ranges, p from sparse to every element (several rounds of two elements per
+    lane), bit-identical to the tile-gather form with the list and to the oracle."""
+    from gym_amd import ops
+    n = 100_003
+    x = np.random.default_rng(K * 7 + ld).standard_normal((K, n)).astype(np.float32)
+    skip = [(0, 3), (640, 700), (50_000, 50_064), (99_990, 100_003)]
+    sk = torch.tensor(skip, dtype=torch.int64, device=DEV)
+    seed, it = 5, 11
+    m = osparta.philox_mask(n, seed, it, p, skip=skip)
+    bufs = []
+    for with_list in (False, True):
+        buf = torch.full((n, ld), 3.0, device=DEV, dtype=dtype)
+        buf[:, :K] = t(np.ascontiguousarray(x.T), dtype)
+        kw = {}
+        if with_list:
+            cap = int(m.sum()) + 8
+            idx, count, work = _sparta_buffers(n, cap)
+            kw = dict(idx=idx, vals=torch.empty(cap, device=DEV, dtype=dtype), cap=cap, count=count, work=work)
+        ops.sparta_average_local(buf[:, :K], n, float(K), seed=seed, iteration=it, p=p, skip=sk, layout="elem", **kw)
+        bufs.append(host(buf))
+    assert np.array_equal(bufs[0], bufs[1])
+    xs = bufs[0]  # untouched elements keep their (dtype-rounded) inputs
+    want = osparta.sparse_average(list(t(np.ascontiguousarray(x.T), dtype).float().cpu().numpy().T), m)
+    tol = 1e-2 if dtype == torch.bfloat16 else 0
+    np.testing.assert_allclose(xs[:, :K].T, np.stack(want), rtol=tol, atol=tol)
+    assert (xs[:, K:] == 3.0).all()

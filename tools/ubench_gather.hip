@@ -55,6 +55,40 @@ __global__ __launch_bounds__(256) void read_tiles(const float* a, long ld, const
     for (int j = threadIdx.x; j < c; j += 256) out[b + j] = acc[j & 511];
 }
 
+// Line-granular forms for the element-major [n, 32] set (round 2): one selected
+// element's 32 fp32 replicas are one 128-B line = 8 lanes x 16 B.  Flat over the
+// M*8 quads (grid-stride) or one workgroup per 16384-element tile.  RMW reads and
+// writes each line once; the read form sums the line (no write).
+__global__ __launch_bounds__(256) void rmw_lines_flat(float4* a, const int* pos, long M) {
+    const long tot = M * 8;
+    for (long f = (long)blockIdx.x * 256 + threadIdx.x; f < tot; f += (long)gridDim.x * 256) {
+        float4* q = a + (long)pos[f >> 3] * 8 + (f & 7);
+        float4 v = *q;
+        v.x = v.x * 0.5f + 1.f; v.y = v.y * 0.5f + 1.f; v.z = v.z * 0.5f + 1.f; v.w = v.w * 0.5f + 1.f;
+        *q = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void rmw_lines_tiles(float4* a, const int* pos, const int* tile_start) {
+    const int b = tile_start[blockIdx.x], c = tile_start[blockIdx.x + 1] - b;
+    for (int f = threadIdx.x; f < c * 8; f += 256) {
+        float4* q = a + (long)pos[b + (f >> 3)] * 8 + (f & 7);
+        float4 v = *q;
+        v.x = v.x * 0.5f + 1.f; v.y = v.y * 0.5f + 1.f; v.z = v.z * 0.5f + 1.f; v.w = v.w * 0.5f + 1.f;
+        *q = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void read_lines_flat(const float4* a, const int* pos, long M, float* out) {
+    const long tot = M * 8;
+    float s = 0.f;
+    for (long f = (long)blockIdx.x * 256 + threadIdx.x; f < tot; f += (long)gridDim.x * 256) {
+        const float4 v = a[(long)pos[f >> 3] * 8 + (f & 7)];
+        s += v.x + v.y + v.z + v.w;
+    }
+    if (s == 12345.f) out[0] = s;
+}
+
 template <typename F>
 float time_ms(F f, int reps) {
     hipEvent_t e0, e1;
@@ -110,6 +144,29 @@ int main() {
     }
     rep("rmw tile-grouped", time_ms([&] { rmw_tiles<<<(unsigned)tiles, 256>>>(a, ld, dpos, dts, K); }, reps), 1);
     rep("read tile-grouped", time_ms([&] { read_tiles<<<(unsigned)tiles, 256>>>(a, ld, dpos, dts, K, out); }, reps), 0);
+    // element-major [n, 32] lines (the same buffer viewed as n rows of 32 floats)
+    std::vector<int> ts16((n + 16383) / 16384 + 1, 0);
+    for (long j = 0, t = 0; t < (long)ts16.size() - 1; ++t) {
+        while (j < M && pos[j] < (t + 1) * 16384) ++j;
+        ts16[t + 1] = (int)j;
+    }
+    int* dts16;
+    CK(hipMalloc(&dts16, sizeof(int) * ts16.size()));
+    CK(hipMemcpy(dts16, ts16.data(), sizeof(int) * ts16.size(), hipMemcpyHostToDevice));
+    const double line_bytes = (double)M * 128;
+    auto repl = [&](const char* name, float ms, int rw) {
+        printf("%-28s %.4f ms  %.0f GB/s of 128-B lines (%s)\n", name, ms, line_bytes * (rw ? 2 : 1) / ms / 1e6,
+               rw ? "read + write" : "read");
+    };
+    float4* a4 = reinterpret_cast<float4*>(a);
+    for (int g : {4096, 16384, 65536}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "lines rmw flat g=%d", g);
+        repl(nm, time_ms([&] { rmw_lines_flat<<<g, 256>>>(a4, dpos, M); }, reps), 1);
+        snprintf(nm, sizeof nm, "lines read flat g=%d", g);
+        repl(nm, time_ms([&] { read_lines_flat<<<g, 256>>>(a4, dpos, M, out); }, reps), 0);
+    }
+    repl("lines rmw 16384-tiles", time_ms([&] { rmw_lines_tiles<<<(unsigned)ts16.size() - 1, 256>>>(a4, dpos, dts16); }, reps), 1);
     CK(hipFree(a));
     return 0;
 }
