@@ -8,11 +8,17 @@ local_step % H == 0 and local_step > 0.
 
 Full averaging is one RCCL all-reduce over the parameter arena plus one
 division kernel (the reference: a per-tensor all-reduce + divide).  Island
-averaging keeps the reference's algorithm — rank 0 shuffles the ranks with
-Python's `random` and broadcasts the permutation (:27-51), every node
-all-gathers the parameters and averages its island's members in ascending
-rank order (:61-69) — as ONE all-gather of the arena and one
-ga_replica_mean over the member rows.
+averaging keeps the reference's partner draw — rank 0 shuffles the ranks with
+Python's `random` and broadcasts the permutation (:27-51) — and its
+arithmetic, the island's members summed in ascending rank order and divided
+(:61-69), but moves only the island's arenas: each island is a sub-
+communicator (`dist.new_group`, created once per distinct member set, by
+every rank in permutation order, and cached), the members all-gather their
+arenas within it ((s-1)·N received per rank instead of the reference's
+(K-1)·N per-tensor all-gather over the world), and one ga_replica_mean over
+the gathered rows averages them.  With a caller-supplied process group the
+island step falls back to one all-gather over that group + the same mean over
+the member rows.
 """
 import random
 from typing import Optional, Set, Union
@@ -21,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..comm import Collective
 from ..engine import MeanReduce
 from .communicate_optimize_strategy import CommunicateOptimizeStrategy, CommunicationModule
 from .optim import OptimSpec
@@ -32,6 +39,8 @@ class AveragingCommunicator(CommunicationModule):
         self.island_size = island_size
         self._mean = None
         self._gathered = None
+        self._islands = []     # this communication's islands, in permutation order
+        self._groups = {}      # sorted member tuple -> (process group, Collective or None)
 
     def _select_partners(self, rank: int, num_nodes: int) -> Set[int]:
         ranks = list(range(num_nodes)) if rank == 0 else [None] * num_nodes
@@ -39,11 +48,25 @@ class AveragingCommunicator(CommunicationModule):
             random.shuffle(ranks)
         dist.broadcast_object_list(ranks, src=0)
         size = self.island_size if self.island_size is not None else num_nodes
-        for i in range(0, len(ranks), size):
-            island = set(ranks[i:i + size])
+        self._islands = [set(ranks[i:i + size]) for i in range(0, len(ranks), size)]
+        for island in self._islands:
             if rank in island:
                 return island
         return None
+
+    def _island_collective(self, members: Set[int]):
+        """Collective over `members` (a sub-communicator).  Every island of this
+        communication that is new gets its group here, on every rank, in the
+        permutation order rank 0 broadcast: dist.new_group is collective over
+        the world, so all ranks create the same groups in the same order."""
+        me = dist.get_rank()
+        for island in self._islands:
+            key = tuple(sorted(island))
+            if len(key) > 1 and key not in self._groups:
+                g = dist.new_group(list(key))
+                self._groups[key] = (g, Collective(g) if me in island else None)
+        key = tuple(sorted(members))
+        return self._groups[key][1] if len(key) > 1 else None
 
     def _average_models(self, model, island_members: Set[int], num_nodes: int) -> None:
         s = self.strategy
@@ -54,11 +77,22 @@ class AveragingCommunicator(CommunicationModule):
                 self._mean = MeanReduce(s.coll, 1, a.n, a.device, a.dtype)
             self._mean(a.flat.view(1, -1))
             return
-        if self._gathered is None:
-            self._gathered = torch.empty(s.coll.world, a.n, device=a.device, dtype=a.dtype)
-        s.coll.all_gather_into(self._gathered.view(-1), a.flat)
-        rows = torch.tensor(sorted(island_members), dtype=torch.int32, device=a.device)
-        ops.replica_mean(self._gathered, a.flat, n=a.n, rows=rows)
+        members = sorted(island_members)
+        coll = self._island_collective(island_members) if s.coll.group is None and self._islands else None
+        if len(members) == 1:  # (0 + x) / 1, as the reference's sum([x]) / 1
+            ops.replica_mean(a.flat.view(1, -1), a.flat, n=a.n)
+            return
+        if coll is not None:
+            rows_all = len(members)
+            rows = None  # every gathered row is a member, in ascending rank order
+        else:
+            coll, rows_all = s.coll, s.coll.world
+            rows = torch.tensor(members, dtype=torch.int32, device=a.device)
+        if self._gathered is None or self._gathered.shape[0] < rows_all:
+            self._gathered = torch.empty(rows_all, a.n, device=a.device, dtype=a.dtype)
+        buf = self._gathered[:rows_all]
+        coll.all_gather_into(buf.view(-1), a.flat)
+        ops.replica_mean(buf, a.flat, n=a.n, rows=rows)
 
     def communicate(self, model, rank: int, num_nodes: int, local_step: int) -> None:
         if num_nodes > 1:

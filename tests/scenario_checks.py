@@ -155,23 +155,33 @@ def check_mnist_diloco(res, world, golden_dir):
 
 
 def check_fedavg(res, world, golden_dir, island_size=None):
+    """Two averaging steps (rank 0's island draws from random.seed(1234)): every
+    node ends at the ascending-rank fp32 mean of its island, bit-exact (the
+    reference's sum(island_tensors) / len, federated_averaging.py:61-69)."""
     nt = 3
-    before = [[res[r][f"before_{i}"] for i in range(nt)] for r in range(world)]
+    state = [[res[r][f"before_{i}"] for i in range(nt)] for r in range(world)]
     for r in range(world):
         for i in range(nt):
-            assert np.array_equal(res[r][f"after0_{i}"], before[r][i])  # local_step 0: no averaging
-    if island_size is None or island_size >= world:
-        islands = [set(range(world))]
-    else:
-        rng = random.Random(1234)
-        ranks = list(range(world))
-        rng.shuffle(ranks)
-        islands = [set(ranks[j:j + island_size]) for j in range(0, world, island_size)]
-    for r in range(world):
-        isl = next(s for s in islands if r in s)
-        for i in range(nt):
-            want = oreduce.mean_reduce([before[m][i] for m in sorted(isl)])
-            np.testing.assert_allclose(res[r][f"after1_{i}"], want, rtol=1e-6, atol=1e-9)
+            assert np.array_equal(res[r][f"after0_{i}"], state[r][i])  # local_step 0: no averaging
+    rng = random.Random(1234)
+    for step in (1, 2):
+        if island_size is None or island_size >= world:
+            islands = [set(range(world))]
+        else:
+            ranks = list(range(world))
+            rng.shuffle(ranks)
+            islands = [set(ranks[j:j + island_size]) for j in range(0, world, island_size)]
+        new = []
+        for r in range(world):
+            isl = next(s for s in islands if r in s)
+            new.append([oreduce.mean_reduce([state[m][i] for m in sorted(isl)]) for i in range(nt)])
+            for i in range(nt):
+                got = res[r][f"after{step}_{i}"]
+                if island_size is None or island_size >= world:
+                    np.testing.assert_allclose(got, new[r][i], rtol=1e-6, atol=1e-9)  # all-reduce order
+                else:
+                    assert np.array_equal(got, new[r][i]), (step, r, i)
+        state = [[res[r][f"after{step}_{i}"] for i in range(nt)] for r in range(world)]
 
 
 def check_demo(res, world, golden_dir):

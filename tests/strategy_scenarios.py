@@ -256,6 +256,9 @@ def sc_fedavg(rank, world, dev, golden_dir, island_size=None):
     s.zero_grad()
     s.step()  # local_step 1: average
     out["after1"] = [_host(p) for p in model.parameters()]
+    s.zero_grad()
+    s.step()  # local_step 2: average again (new islands: new or cached sub-communicators)
+    out["after2"] = [_host(p) for p in model.parameters()]
     return {f"{k}_{i}": v for k, lst in out.items() for i, v in enumerate(lst)}
 
 

@@ -24,7 +24,7 @@ CASES = [
     ("sparta_sel", 3, {"kind": "philox"}),
     ("eval_avg", 2, {}), ("eval_avg", 3, {}),
     ("mnist_diloco", 2, {}),
-    ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}),
+    ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}), ("fedavg", 4, {"island_size": 3}),
     ("demo", 2, {}),
 ]
 
