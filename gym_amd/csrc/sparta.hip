@@ -445,15 +445,12 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
 // Measured (K = 32, 124M, p = 0.005): 0.049-0.053 ms against 0.054-0.063 ms for
 // the 16384-element tile-gather kernel; a persistent form that draws tile t+1's
 // mask while tile t's loads are in flight ran 0.062 / 0.065 / 0.074 ms at 2 / 4 /
-// 8 tiles per wave (fewer waves in flight), and splitting the kernel's work
-// measured mask only 0.015 ms, gather only 0.034 ms.
+// 8 tiles per wave (fewer waves in flight), and builds of the kernel with only
+// its mask (0.015 ms) or only its gather (0.034 ms) add up to the whole.
 constexpr int kWTile = 64 * kSpPerThread;  // elements per wavefront tile
 constexpr int kWList = 256;                // listed positions per window
 #ifndef GA_SP_WAVES
 #define GA_SP_WAVES 4  // wavefronts (independent tiles) per workgroup
-#endif
-#ifndef GA_SP_EXPERIMENT
-#define GA_SP_EXPERIMENT 0  // timing experiments (tools/ab_sparta_wave.sh): 1 mask only, 2 gather only
 #endif
 
 // orders this wave's LDS accesses (the wave is the only writer of its slices)
@@ -523,15 +520,7 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(P
     const int64_t t = (int64_t)blockIdx.x * GA_SP_WAVES + wid;
     const int64_t tile0 = t * kWTile;
     const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
-#if GA_SP_EXPERIMENT == 2  // no mask: a fixed ~20-per-wave pattern (timing experiment only)
-    const uint64_t bits = (e0 < n && lane % 3 == 0) ? 1ull << (t % 64) : 0ull;
-#else
     const uint64_t bits = e0 < n ? pred_bits64(P, tab, e0, n) : 0ull;
-#endif
-#if GA_SP_EXPERIMENT == 1  // mask only, no gather (timing experiment only)
-    if (__popcll(bits) == 1000) src[0] = (T)0.f;
-    return;
-#endif
     const int c = __popcll(bits);
     int x = c;
 #pragma unroll
