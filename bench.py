@@ -139,6 +139,29 @@ class KernelTimer:
         return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else None
 
 
+def queued_ms(fn, reps, dev, fill_bytes=1 << 30, fills=4):
+    """GPU time per call of fn with its launches queued back to back: streaming
+    copies (ga_stream_copy, ~1.5 ms) occupy the GPU while the host enqueues the
+    reps calls, so the two events bracket GPU work only, not the host's launch
+    gaps.  For kernels of tens of microseconds, where HIP events around one
+    launch measure the host's launch latency as much as the kernel."""
+    a = torch.empty(fill_bytes // 4, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(0.0)
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(fills):
+        ops.stream_copy(a, b)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    del a, b
+    return e0.elapsed_time(e1) / reps
+
+
 def host_cores():
     """CPU share of this process: the job's thread budget (OMP_NUM_THREADS is
     set to the box's share on the GPU pool), capped by the visible CPUs."""
@@ -277,13 +300,17 @@ def bench_diloco(args, coll, dev):
     return out
 
 
-def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout_kind="elem"):
+def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout_kind="elem", mask_source="philox"):
     """configs[3]: K=32 simulated nodes on one GPU, or the same 32 nodes sharded
     32/G per GPU over G GPUs (strong: the node count is the config's).
     layout_kind "elem": the replica set element-major [n, K] (one element's K
     replicas adjacent: at K=32 fp32 one 128-B line per selected element);
     "rows": [K, n], the replica training loop's layout (every selected
-    (element, replica) a separate random 4-B word)."""
+    (element, replica) a separate random 4-B word).
+    mask_source "philox": the in-kernel stream (the fast mode); "torch": the
+    reference's per-tensor torch.bernoulli draws (the drop-in default,
+    bit-identical selections) into a uint8 mask arena inside the timed step,
+    packed and broadcast from rank 0 at N > 1."""
     K = max(1, K_total // coll.world)
     shapes = MODELS[model]()
     layout = ArenaLayout(shapes)
@@ -305,9 +332,19 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     avg_local = ops.sparta_average_local
     ops.sparta_average_local = timer.wrap(avg_local)
     it = [0]
+    if mask_source == "torch":
+        from gym_amd.strategy.sparta import RandomIndexSelector, draw_masks
+        sel, pfull = RandomIndexSelector(p), []
+        mask = torch.zeros(layout.n, dtype=torch.uint8, device=dev)
+        mviews = layout.views(mask)
+        torch.manual_seed(42)
 
     def step():
-        eng(reps, seed=42, iteration=it[0])
+        if mask_source == "torch":
+            draw_masks(sel, mviews, mviews, set(), it[0], pfull)
+            eng(reps, mask=mask, mask_cap=eng.cap)
+        else:
+            eng(reps, seed=42, iteration=it[0])
         it[0] += 1
 
     timer.on = True
@@ -316,6 +353,9 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     finally:
         ops.sparta_average_local = avg_local
     kern = timer.mean_ms()
+    # events around single launches measure host launch latency at this size; the
+    # queued form brackets GPU work only (agrees with rocprofv3's kernel durations)
+    queued = queued_ms(step, args.steps, dev) if coll.world == 1 and mask_source == "philox" else None
     eng.check()
     # the number selected (untimed; the fused single-GPU pass produces no list)
     ops.sparta_select(reps, layout.n, eng.cap, eng.idx, eng.vals, eng.count, eng.work, seed=42, iteration=0, p=p,
@@ -333,8 +373,18 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
            "alg_GBps": round(alg / t / 1e9, 1), "sector_bytes": sect, "sector_GBps": round(sect / t / 1e9, 1),
            "sector_over_alg": round(sect / max(alg, 1), 3),
            "path": "fused select+gather+average+write-back" if coll.world == 1 else
-                   f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter"}
-    if kern is not None:
+                   f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter",
+           "mask_source": mask_source}
+    if mask_source == "torch":
+        out["mask"] = ("reference per-tensor torch.bernoulli draws (148 launches) into a uint8 arena, in the step" +
+                       ("" if coll.world == 1 else f"; rank 0's packed to bits and broadcast: "
+                        f"{ops.sparta_mask_words(layout.n) * 8 + 8} B instead of {layout.n} B"))
+    if queued is not None:
+        out["kernel_ms"] = round(queued, 4)
+        out["kernel_alg_GBps"] = round(alg / (queued * 1e-3) / 1e9, 1)
+        out["kernel_frac_hbm"] = round(alg / (queued * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        out["kernel_ms_single_launch_events"] = round(kern, 4) if kern is not None else None
+    elif kern is not None:
         out["kernel_ms"] = round(kern, 4)
     if conv_ms is not None:
         out["rows_to_elem_transpose_ms"] = round(conv_ms, 3)
@@ -350,8 +400,14 @@ def bench_simple(args, coll, dev, K_total=8, model="gpt2-char"):
     rs = synth_replicas(layout, K, coll.rank, dev)
     eng = MeanReduce(coll, K, layout.n, dev, torch.float32)
     t = timed_loop(lambda: eng(rs.data), args.steps, args.warmup, coll)
-    return {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
-            "K_local": K, "K_total": K * coll.world, "model": model}
+    out = {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
+           "K_local": K, "K_total": K * coll.world, "model": model}
+    if coll.world == 1:  # one ga_replica_mean launch: read K replicas, write K
+        q = queued_ms(lambda: eng(rs.data), args.steps, dev)
+        alg = 2 * K * 4 * layout.n
+        out.update({"kernel_ms": round(q, 4), "kernel_alg_GBps": round(alg / (q * 1e-3) / 1e9, 1),
+                    "kernel_frac_hbm": round(alg / (q * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+    return out
 
 
 def bench_demo(args, coll, dev, model="gpt2-350m"):
@@ -522,6 +578,7 @@ def main():
     if not args.no_extras and args.only != "diloco":
         runs = [("sparta_k32", bench_sparta),
                 ("sparta_k32_rows", lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows")),
+                ("sparta_k32_torch_mask", lambda a, c, d: bench_sparta(a, c, d, mask_source="torch")),
                 ("simple_reduce_char_k8", bench_simple),
                 ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
         if coll.world == 1:

@@ -18,6 +18,8 @@ GA_F32 = 0
 GA_BF16 = 1
 GA_LAYOUT_ROWS = 0
 GA_LAYOUT_ELEM_MAJOR = 1
+GA_MASK_BYTES = 0
+GA_MASK_BITS = 1
 
 c_i32, c_i64, c_u32, c_u64, c_f32, c_f64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_float, ctypes.c_double)
@@ -52,11 +54,12 @@ SIGNATURES = {
                                 c_f32, c_f32, c_i32, c_p, c_i64, c_i64, c_p]),
     "ga_sparta_workspace_bytes": (c_i64, [c_i64]),
     "ga_sparta_gap_table": (None, [c_f64, c_p]),
-    "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_f64, c_p, c_i64, c_i64,
-                                 c_p, c_p, c_p, c_p, c_p]),
+    "ga_sparta_pack_mask": (c_i32, [c_p, c_i64, c_p, c_p]),
+    "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_i32, c_u64, c_u64, c_f64, c_p, c_i64,
+                                 c_i64, c_p, c_p, c_p, c_p, c_p]),
     "ga_sparta_scatter": (c_i32, [c_i32, c_p, c_p, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_i32, c_p]),
-    "ga_sparta_average_local": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_u64, c_u64, c_f64, c_p, c_i64,
-                                        c_f32, c_p, c_p, c_i64, c_p, c_p, c_p]),
+    "ga_sparta_average_local": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_i32, c_u64, c_u64, c_f64, c_p,
+                                        c_i64, c_f32, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "ga_demo_tensor_bytes": (c_i32, []),
     "ga_demo_encode": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32,
                                c_f32, c_p, c_i64, c_i64, c_p]),

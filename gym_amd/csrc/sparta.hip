@@ -5,7 +5,9 @@
 // Selection is a stream compaction in ascending element order, so the packed
 // order equals `param.data[mask]` over the concatenated parameters
 // (sparta.py:38).  The mask is either a uint8 arena (rank 0's mask, exactly
-// the reference semantics) or generated in-kernel from Philox4x32-10 keyed by
+// the reference semantics), the same mask packed to one bit per element
+// (ga_sparta_pack_mask: what crosses the wire at N > 1, n/8 bytes instead of
+// n) or generated in-kernel from Philox4x32-10 keyed by
 // (seed, iteration) -- then every rank derives the same mask and nothing is
 // broadcast.  Three passes: per-tile count, one-block scan of tile counts,
 // select+gather (the predicate is recomputed).
@@ -49,7 +51,8 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 }
 
 struct Pred {
-    const uint8_t* mask;  // null -> Philox
+    const uint8_t* mask;  // uint8 mask arena, or null
+    const uint64_t* bits; // packed mask (bit j of word w = element 64 w + j), or null; both null -> Philox
     uint2 key;
     uint32_t it_lo, it_hi;
     const int64_t* skip;  // Philox: sorted disjoint [lo, hi) element ranges never selected
@@ -91,6 +94,10 @@ __device__ __forceinline__ int gap_of(const uint64_t* tab, uint32_t u) {
 // tab: the gap table in LDS.
 __device__ __forceinline__ uint64_t pred_bits64(const Pred& P, const uint64_t* tab, int64_t e0, int64_t n) {
     uint64_t bits = 0;
+    if (P.bits) {
+        bits = P.bits[e0 >> 6];
+        return e0 + 64 <= n ? bits : bits & ((1ull << (n - e0)) - 1ull);
+    }
     if (P.mask) {
         if (e0 + 64 <= n) {
 #pragma unroll
@@ -622,6 +629,30 @@ static void launch_scatter(dim3 grid, hipStream_t stream, const void* vals, cons
     }
 }
 
+// uint8 mask arena -> one bit per element (bit j of word w = mask[64 w + j] != 0;
+// bits past n are 0): one lane per 64-element word, the mask read as 4 x 16 B
+__global__ __launch_bounds__(kSpBlock) void sparta_pack_mask_kernel(const uint8_t* __restrict__ mask, int64_t n,
+                                                                    uint64_t* __restrict__ bits) {
+    const int64_t w = (int64_t)blockIdx.x * kSpBlock + threadIdx.x;
+    const int64_t e0 = w * 64;
+    if (e0 >= n) return;
+    uint64_t b = 0;
+    if (e0 + 64 <= n) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint4 m = *reinterpret_cast<const uint4*>(mask + e0 + 16 * v);
+            const uint32_t q[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b |= (uint64_t)(((q[i] >> (8 * j)) & 0xffu) != 0u) << (16 * v + 4 * i + j);
+        }
+    } else {
+        for (int j = 0; e0 + j < n; ++j) b |= (uint64_t)(mask[e0 + j] != 0) << j;
+    }
+    bits[w] = b;
+}
+
 static int64_t sparta_tiles(int64_t n) { return ceil_div(n, kSpTile); }
 
 static Rep make_rep(int64_t ld, int layout) {
@@ -681,10 +712,11 @@ extern "C" GA_API void ga_sparta_gap_table(double p, uint64_t* table) {
     }
 }
 
-static Pred make_pred(const uint8_t* mask, uint64_t seed, uint64_t iteration, double p, const int64_t* skip,
-                      int64_t nskip) {
+static Pred make_pred(const void* mask, int mask_format, uint64_t seed, uint64_t iteration, double p,
+                      const int64_t* skip, int64_t nskip) {
     Pred P;
-    P.mask = mask;
+    P.mask = mask_format == GA_MASK_BYTES ? (const uint8_t*)mask : nullptr;
+    P.bits = mask_format == GA_MASK_BITS ? (const uint64_t*)mask : nullptr;
     P.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
     P.it_lo = (uint32_t)iteration;
     P.it_hi = (uint32_t)(iteration >> 32);
@@ -695,7 +727,7 @@ static Pred make_pred(const uint8_t* mask, uint64_t seed, uint64_t iteration, do
 }
 
 extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld, int layout, int64_t n,
-                                       const uint8_t* mask, uint64_t seed, uint64_t iteration,
+                                       const void* mask, int mask_format, uint64_t seed, uint64_t iteration,
                                        double p, const int64_t* skip, int64_t nskip,
                                        int64_t cap, int32_t* idx, void* vals,
                                        int64_t* count, void* work, hipStream_t stream) {
@@ -706,11 +738,13 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_select: bad layout %d", layout);
     GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_select: ld too small");
     GA_REQUIRE(p >= 0.0 && p <= 1.0, "ga_sparta_select: p=%g outside [0, 1]", p);
+    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS, "ga_sparta_select: bad mask_format %d",
+               mask_format);
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_select: mask must be 16-byte aligned");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_select: bad skip table");
     if (n == 0) return hipMemsetAsync(count, 0, 2 * sizeof(int64_t), stream) == hipSuccess ? GA_OK : GA_EHIP;
     GA_REQUIRE(src && idx && vals, "ga_sparta_select: null src/idx/vals");
-    const Pred P = make_pred(mask, seed, iteration, p, skip, nskip);
+    const Pred P = make_pred(mask, mask_format, seed, iteration, p, skip, nskip);
     switch (dtype) {
         case GA_F32:
             return launch_select<float>(src, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work, 0.f, stream);
@@ -722,8 +756,8 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
 }
 
 extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int layout, int64_t n,
-                                              const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                              double p, const int64_t* skip, int64_t nskip,
+                                              const void* mask, int mask_format, uint64_t seed,
+                                              uint64_t iteration, double p, const int64_t* skip, int64_t nskip,
                                               float divisor, int32_t* idx, void* vals,
                                               int64_t cap, int64_t* count, void* work, hipStream_t stream) {
     clear_error();
@@ -733,13 +767,15 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
     GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_average_local: bad layout");
     GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_average_local: ld too small");
     GA_REQUIRE(p >= 0.0 && p <= 1.0, "ga_sparta_average_local: p=%g outside [0, 1]", p);
+    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS,
+               "ga_sparta_average_local: bad mask_format %d", mask_format);
     GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_average_local: mask alignment");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_average_local: bad skip table");
     GA_REQUIRE((idx == nullptr && vals == nullptr && count == nullptr) || (idx && vals && count && work),
                "ga_sparta_average_local: idx, vals, count and work go together");
     if (n == 0) return GA_OK;
     GA_REQUIRE(reps, "ga_sparta_average_local: null replicas");
-    const Pred P = make_pred(mask, seed, iteration, p, skip, nskip);
+    const Pred P = make_pred(mask, mask_format, seed, iteration, p, skip, nskip);
     switch (dtype) {
         case GA_F32:
             return launch_select<float>(reps, K, make_rep(ld, layout), n, P, cap, idx, vals, count, work, divisor,
@@ -749,6 +785,18 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
                                                  divisor, stream);
         default: set_error("ga_sparta_average_local: unknown dtype %d", dtype); return GA_EINVAL;
     }
+}
+
+extern "C" GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(n >= 0, "ga_sparta_pack_mask: n=%lld", (long long)n);
+    if (n == 0) return GA_OK;
+    GA_REQUIRE(mask && bits, "ga_sparta_pack_mask: null mask/bits");
+    GA_REQUIRE(((uintptr_t)mask % 16) == 0 && ((uintptr_t)bits % 8) == 0, "ga_sparta_pack_mask: alignment");
+    const int64_t words = ceil_div(n, (int64_t)64);
+    hipLaunchKernelGGL(sparta_pack_mask_kernel, dim3((unsigned)ceil_div(words, (int64_t)kSpBlock)), dim3(kSpBlock), 0,
+                       stream, mask, n, bits);
+    return check_launch("ga_sparta_pack_mask");
 }
 
 extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx, const int64_t* count,

@@ -253,6 +253,7 @@ class Sparta:
         self.work = ops.sparta_workspace(n, device)
         self._flag_host = torch.zeros(2, dtype=torch.int64, pin_memory=torch.cuda.is_available())
         self._flag_event = None
+        self.bits = None  # packed mask broadcast buffer (mask mode with an exchange)
 
     def _ensure_cap(self, cap):
         if cap > self.cap:
@@ -273,13 +274,36 @@ class Sparta:
             if int(self._flag_host[1]) != 0:
                 raise RuntimeError(f"SPARTA: {int(self._flag_host[0])} elements selected > capacity {self.cap}")
 
-    def __call__(self, reps, seed=0, iteration=0, mask=None, skip=None):
+    def __call__(self, reps, seed=0, iteration=0, mask=None, skip=None, mask_cap=None):
+        """mask: this process's uint8/bool mask arena (the reference selector's
+        draws) or None for the Philox stream.  With an exchange, rank 0's mask
+        wins (sparta.py:32-37): it is packed to one bit per element and
+        broadcast (n/8 bytes; every rank's own draw is overwritten).
+        mask_cap: a bound on the selected count that holds on every rank (e.g.
+        sparta_capacity for Bernoulli masks): no host sync for the exact count,
+        overflow flagged on the device as in Philox mode.  None: the exact
+        count is read back (any selector)."""
         n = self.n
-        if mask is not None:  # reference mask (rank 0's); exact count known from the mask
-            cap = max(1, int(mask[:n].sum().item()))
+        cnt = None
+        if mask is not None and self.coll.exchange:
+            words = ops.sparta_mask_words(n)
+            if self.bits is None:  # the packed words + rank 0's selected count in the last word
+                self.bits = torch.empty(words + 1, dtype=torch.int64, device=self.device)
+            ops.sparta_pack_mask(mask, n, self.bits)
+            if mask_cap is None:
+                self.bits[words:].copy_(mask[:n].sum(dtype=torch.int64).view(1))
+            self.coll.broadcast_(self.bits, 0)
+            mask = self.bits[:words]
+            if mask_cap is None:
+                cnt = self.bits[words]
+        if mask is not None and mask_cap is None:  # exact count known from the mask
+            cnt = mask[:n].sum() if cnt is None else cnt
+            cap = max(1, int(cnt.item()))
             self._ensure_cap(cap)
             cap_used = cap
         else:
+            if mask is not None:
+                self._ensure_cap(int(mask_cap))
             self.check()
             cap_used = self.cap
         if not self.coll.exchange:  # every node is a local replica: one fused pass, no exchange
@@ -290,7 +314,7 @@ class Sparta:
                           iteration=iteration, p=self.p, skip=skip, layout=self.layout)
         self.coll.all_reduce_(self.vals[:cap_used])
         ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps, layout=self.layout)
-        if mask is None:  # overflow flag read back asynchronously, checked next step
+        if mask is None or mask_cap is not None:  # overflow flag read back asynchronously, checked next step
             self._flag_host.copy_(self.count, non_blocking=True)
             if self.device.type == "cuda":
                 self._flag_event = torch.cuda.Event()

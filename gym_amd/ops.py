@@ -114,6 +114,38 @@ def _rate(p, mask):
     return p
 
 
+def sparta_mask_words(n):
+    """int64 words of a packed SPARTA mask of n elements (ga_sparta_pack_mask)."""
+    return (int(n) + 63) // 64
+
+
+def sparta_pack_mask(mask, n, bits):
+    """bits (int64 [>= ceil(n/64)]) <- the uint8/bool mask arena packed one bit
+    per element (bit j of word w = element 64 w + j)."""
+    _gpu(mask, bits)
+    if mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n or not mask.is_contiguous():
+        raise ValueError("sparta_pack_mask: mask must be a contiguous uint8/bool tensor with >= n elements")
+    if bits.dtype != torch.int64 or bits.numel() < sparta_mask_words(n) or not bits.is_contiguous():
+        raise ValueError("sparta_pack_mask: bits must be a contiguous int64 tensor of >= ceil(n/64) words")
+    check(lib().ga_sparta_pack_mask(_p(mask), int(n), _p(bits), _stream()), "ga_sparta_pack_mask")
+
+
+def _mask_arg(mask, n, who):
+    """(mask, format code) of a SPARTA mask: uint8/bool per element, or int64
+    packed words (sparta_pack_mask)."""
+    if mask is None:
+        return None, _lib.GA_MASK_BYTES
+    if mask.dtype in (torch.uint8, torch.bool):
+        if mask.numel() < n:
+            raise ValueError(f"{who}: mask must have >= n elements")
+        return mask, _lib.GA_MASK_BYTES
+    if mask.dtype == torch.int64:
+        if mask.numel() < sparta_mask_words(n):
+            raise ValueError(f"{who}: packed mask must have >= ceil(n/64) words")
+        return mask, _lib.GA_MASK_BITS
+    raise ValueError(f"{who}: mask must be uint8/bool (per element) or int64 (packed words)")
+
+
 def sparta_workspace(n, device):
     nbytes = int(lib().ga_sparta_workspace_bytes(int(n)))
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -163,11 +195,10 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
         raise ValueError("sparta_select: idx/vals smaller than cap")
     if work.numel() < lib().ga_sparta_workspace_bytes(int(n)):
         raise ValueError("sparta_select: workspace too small")
-    if mask is not None:
-        if mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n:
-            raise ValueError("sparta_select: mask must be uint8/bool with >= n elements")
+    mask, mfmt = _mask_arg(mask, n, "sparta_select")
     thr = _rate(p, mask)
-    check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, code, int(n), _p(mask), int(seed) & (2**64 - 1),
+    check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, code, int(n), _p(mask), mfmt,
+                                 int(seed) & (2**64 - 1),
                                  int(iteration) & (2**64 - 1), thr, _p(skip), nskip, int(cap), _p(idx), _p(vals),
                                  _p(count),
                                  _p(work), _stream()), "ga_sparta_select")
@@ -183,15 +214,14 @@ def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0
     if _rows_of(r2, code) < n:
         raise ValueError("sparta_average_local: replica set shorter than n")
     skip, nskip = _skip_table(skip)
-    if mask is not None and (mask.dtype not in (torch.uint8, torch.bool) or mask.numel() < n):
-        raise ValueError("sparta_average_local: mask must be uint8/bool with >= n elements")
+    mask, mfmt = _mask_arg(mask, n, "sparta_average_local")
     if idx is not None:
         if idx.dtype != torch.int32 or vals.dtype != r2.dtype or count.dtype != torch.int64:
             raise TypeError("sparta_average_local: idx int32, vals arena dtype, count int64")
         if idx.numel() < cap or vals.numel() < cap or work.numel() < lib().ga_sparta_workspace_bytes(int(n)):
             raise ValueError("sparta_average_local: output buffers too small")
     thr = _rate(p, mask)
-    check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, code, int(n), _p(mask),
+    check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, code, int(n), _p(mask), mfmt,
                                         int(seed) & (2**64 - 1),
                                         int(iteration) & (2**64 - 1), thr, _p(skip), nskip, float(divisor),
                                         _p(idx), _p(vals),

@@ -33,7 +33,7 @@ from .fused_optim import ArenaAdam, fusable
 from .strategy.demo import DeMoStrategy
 from .strategy.diloco import DiLoCoStrategy, fused_sgd_hparams
 from .strategy.federated_averaging import FedAvgStrategy
-from .strategy.sparta import RandomIndexSelector, SPARTAStrategy
+from .strategy.sparta import RandomIndexSelector, SPARTAStrategy, draw_masks
 from .strategy.strategy import SimpleReduceStrategy, clip_arena_grad_norm_
 
 
@@ -136,6 +136,7 @@ class ReplicaRunner:
                     self.seed = int(t.item())
                 else:
                     self.mask = torch.zeros(ld, dtype=torch.uint8, device=dev)
+                    self.pfull = []
                 self.iteration = 0
         # the strategy's LR schedule on every optimizer (strategy.py:75-112)
         for o in (self.optim.opts if isinstance(self.optim, _PerNodeOptim) else [self.optim]):
@@ -171,7 +172,9 @@ class ReplicaRunner:
             if self.philox:
                 self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
             else:
-                self.sparta(P, mask=self._build_mask())
+                sel = s.index_selector
+                self.sparta(P, mask=self._build_mask(),
+                            mask_cap=self.sparta.cap if type(sel) is RandomIndexSelector else None)
             self.iteration += 1
         elif isinstance(s, FedAvgStrategy):
             self._inner()
@@ -202,15 +205,11 @@ class ReplicaRunner:
 
     def _build_mask(self):
         """Node 0's selector masks (the reference broadcasts rank 0's,
-        sparta.py:32-37) as one uint8 arena, broadcast to the other processes."""
+        sparta.py:32-37) as one uint8 arena; the engine packs the first
+        process's and broadcasts it to the others."""
         a0 = self.ra.arenas[0]
-        skip = set(self._grad_less())
-        for i, (p, v) in enumerate(zip(a0.params, self.ra.layout.views(self.mask))):
-            if i in skip:
-                v.zero_()
-            else:
-                v.copy_(self.s.index_selector.get_indices(p, self.iteration))
-        self.coll.broadcast_(self.mask, 0)
+        draw_masks(self.s.index_selector, a0.params, self.ra.layout.views(self.mask), set(self._grad_less()),
+                   self.iteration, self.pfull)
         return self.mask
 
     def _inner(self):

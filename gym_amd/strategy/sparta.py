@@ -17,8 +17,9 @@ mask_source=...)):
   "torch" (default) — the reference's exact draw,
       torch.bernoulli(torch.full(shape, p, device=param.device)) per tensor in
       parameter order (same generator calls, so the same selections and the
-      same global RNG state afterwards), rank 0's masks broadcast as one uint8
-      mask arena.  Bit-identical to the reference given the same generator.
+      same global RNG state afterwards), rank 0's masks broadcast as one mask
+      arena packed to a bit per element (n/8 bytes instead of the reference's
+      n bool bytes).  Bit-identical to the reference given the same generator.
   "philox" (opt-in fast mode) — each element is selected independently with
       probability p, drawn in-kernel as the Geometric(p) gaps between selected
       elements from Philox4x32-10 keyed by a per-run seed (rank 0's
@@ -59,6 +60,32 @@ class RandomIndexSelector(IndexSelector):
 
     def get_indices(self, param, iteration):
         return torch.bernoulli(torch.full(param.shape, self.p, device=param.device)).bool()
+
+
+def draw_masks(selector, params, views, skip, iteration, pfull):
+    """Every tensor's selector mask into its view of a uint8 mask arena, in
+    parameter order (sparta.py:28-33); tensors in `skip` stay 0.
+
+    RandomIndexSelector: `view.bernoulli_(P)` with P = the cached
+    torch.full(shape, p) of the tensor -- the same bernoulli kernel on the same
+    probabilities as the reference's torch.bernoulli(torch.full(shape, p))
+    (so the same bits and the same generator offsets), written straight into
+    the arena: no per-step fill of 4 B/element, no float mask, no copy.
+    pfull: the per-tensor cache (a list, filled here).  Other selectors: their
+    get_indices, copied in."""
+    fast = type(selector) is RandomIndexSelector
+    if fast and len(pfull) != len(params):
+        pfull[:] = [None] * len(params)
+    for i, (p, v) in enumerate(zip(params, views)):
+        if i in skip:
+            v.zero_()
+        elif fast:
+            P = pfull[i]
+            if P is None or P.shape != p.shape or P.device != p.device:
+                P = pfull[i] = torch.full(p.shape, selector.p, device=p.device)
+            v.bernoulli_(P)
+        else:
+            v.copy_(selector.get_indices(p, iteration))
 
 
 class ShuffledSequentialIndexSelector(IndexSelector):
@@ -124,6 +151,7 @@ class SparseCommunicator(CommunicationModule):
         self._mask = None
         self._skip_key = None
         self._skip = None
+        self._pfull = []
 
     def _init_node(self, model, rank, num_nodes):
         pass
@@ -165,19 +193,23 @@ class SparseCommunicator(CommunicationModule):
 
     def _build_mask(self, model):
         """Reference mask path: per-tensor selector draws into one uint8 mask
-        arena (frozen / grad-less tensors stay 0), then rank 0's is broadcast."""
+        arena (frozen / grad-less tensors stay 0); the engine packs rank 0's
+        and broadcasts it."""
         s = self.strategy
         a = s.arena
         if self._mask is None:
             self._mask = torch.zeros(a.n, dtype=torch.uint8, device=a.device)
-        views = a.layout.views(self._mask)
-        for p, v in zip(a.params, views):
-            if not p.requires_grad or p.grad is None:
-                v.zero_()
-                continue
-            v.copy_(self.index_selector.get_indices(p, self.iteration))
-        s.coll.broadcast_(self._mask, 0)
+        skip = {i for i, p in enumerate(a.params) if not p.requires_grad or p.grad is None}
+        draw_masks(self.index_selector, a.params, a.layout.views(self._mask), skip, self.iteration, self._pfull)
         return self._mask
+
+    def _mask_cap(self):
+        """Selected-count bound for Bernoulli masks (no host sync per step);
+        None (exact count read back) for the deterministic-cycle and custom
+        selectors."""
+        if type(self.index_selector) is RandomIndexSelector:
+            return self._engine.cap
+        return None
 
     def finish(self):
         if self._engine is not None:
@@ -194,7 +226,7 @@ class SparseCommunicator(CommunicationModule):
                 if self._philox_mode():
                     self._engine(reps, seed=self._shared_seed(), iteration=self.iteration, skip=self._skip_table())
                 else:
-                    self._engine(reps, mask=self._build_mask(model))
+                    self._engine(reps, mask=self._build_mask(model), mask_cap=self._mask_cap())
         self.iteration += 1
 
 

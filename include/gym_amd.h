@@ -49,6 +49,12 @@ extern "C" {
 #define GA_LAYOUT_ROWS 0
 #define GA_LAYOUT_ELEM_MAJOR 1
 
+/* SPARTA mask formats:
+ *   GA_MASK_BYTES  uint8 per element (selected iff != 0), 16-byte aligned
+ *   GA_MASK_BITS   uint64 words, bit j of word w = element 64 w + j (ga_sparta_pack_mask) */
+#define GA_MASK_BYTES 0
+#define GA_MASK_BITS 1
+
 /* ---- library ---------------------------------------------------------- */
 
 /* ABI version (major*100 + minor). */
@@ -125,12 +131,21 @@ GA_API int64_t ga_sparta_workspace_bytes(int64_t n);
 GA_API void ga_sparta_gap_table(double p, uint64_t* table);
 
 /*
+ * bits[w] = OR_j (mask[64 w + j] != 0) << j over the n-element uint8 mask
+ * arena, ceil(n/64) words, bits past n zero: rank 0's selector masks in the
+ * form they are broadcast at N > 1 (n/8 bytes on the wire instead of the
+ * reference's n bool bytes per step, sparta.py:32-37).
+ */
+GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, hipStream_t stream);
+
+/*
  * Select the SPARTA index set over an arena of n elements and gather the
  * selected values summed over the K local replicas (replica set in `layout`,
  * GA_LAYOUT_*).
- *   mask source: if mask != null, element i is selected iff mask[i] != 0
- *   (uint8 mask arena: rank 0's per-tensor index_selector masks, broadcast --
- *   sparta.py:32-37); otherwise the in-kernel Philox4x32-10 stream decides
+ *   mask source: if mask != null, element i is selected iff its mask entry is
+ *   set (mask_format GA_MASK_BYTES: uint8 mask arena, GA_MASK_BITS: the packed
+ *   words of ga_sparta_pack_mask -- rank 0's per-tensor index_selector masks,
+ *   broadcast, sparta.py:32-37); otherwise the in-kernel Philox4x32-10 stream decides
  *   with selection rate p (see ga_sparta_gap_table), except inside the `nskip` element ranges skip[2r] <= i < skip[2r+1]
  *   (sorted, disjoint: the tensors without a gradient, which the reference
  *   skips, sparta.py:29-30; skip may be null when nskip == 0).
@@ -144,8 +159,8 @@ GA_API void ga_sparta_gap_table(double p, uint64_t* table);
  * broadcast and gather of SparseCommunicator.communicate (sparta.py:24-38).
  */
 GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, int64_t ld,
-                            int layout, int64_t n, const uint8_t* mask, uint64_t seed,
-                            uint64_t iteration, double p,
+                            int layout, int64_t n, const void* mask, int mask_format,
+                            uint64_t seed, uint64_t iteration, double p,
                             const int64_t* skip, int64_t nskip, int64_t cap,
                             int32_t* idx, void* vals, int64_t* count, void* work,
                             hipStream_t stream);
@@ -169,8 +184,8 @@ GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx,
  * ga_sparta_select.  Replaces sparta.py:24-44 for batched replicas.
  */
 GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld, int layout, int64_t n,
-                                   const uint8_t* mask, uint64_t seed, uint64_t iteration,
-                                   double p, const int64_t* skip, int64_t nskip,
+                                   const void* mask, int mask_format, uint64_t seed,
+                                   uint64_t iteration, double p, const int64_t* skip, int64_t nskip,
                                    float divisor, int32_t* idx, void* vals,
                                    int64_t cap, int64_t* count, void* work, hipStream_t stream);
 

@@ -166,3 +166,20 @@ def partitioned_masks(numel, p, rank_orders, calls):
         out.append(parts == cur)
         cur += 1
     return out
+
+
+def pack_mask(mask):
+    """The wire form of a mask arena (gym_amd's ga_sparta_pack_mask, no
+    reference counterpart): bit j of int64 word w = (mask[64 w + j] != 0),
+    ceil(n/64) words, bits past n zero."""
+    m = np.asarray(mask).reshape(-1) != 0
+    words = -(-m.size // 64)
+    pad = np.zeros(words * 64, dtype=bool)
+    pad[:m.size] = m
+    return np.packbits(pad.reshape(words, 64), axis=1, bitorder="little").reshape(-1).view("<i8").copy()
+
+
+def unpack_mask(words, n):
+    """Inverse of pack_mask: the n-element bool mask."""
+    b = np.unpackbits(np.asarray(words, dtype="<i8").view(np.uint8), bitorder="little")
+    return b[:n].astype(bool)

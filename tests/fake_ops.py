@@ -56,6 +56,21 @@ def sparta_workspace(n, device):
     return torch.empty(16, dtype=torch.uint8, device=device)
 
 
+def sparta_mask_words(n):
+    return (int(n) + 63) // 64
+
+
+def sparta_pack_mask(mask, n, bits):
+    bits[:sparta_mask_words(n)] = torch.from_numpy(osparta.pack_mask(_np(mask)[:n]))
+
+
+def _mask_bits(mask, n):
+    """bool numpy mask of n elements from a uint8/bool arena or packed int64 words."""
+    if mask.dtype == torch.int64:
+        return osparta.unpack_mask(mask.cpu().numpy(), n)
+    return _np(mask)[:n] != 0
+
+
 def _skip_list(skip):
     return None if skip is None else [tuple(r) for r in skip.cpu().tolist()]
 
@@ -67,8 +82,8 @@ def _rows_view(t, layout):
 def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iteration=0, p=0.0, skip=None,
                   layout="rows"):
     src = _rows_view(src, layout)
-    m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
-                                                                           skip=_skip_list(skip))
+    m = _mask_bits(mask, n) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
+                                                                         skip=_skip_list(skip))
     sel = np.flatnonzero(m)
     count[0] = len(sel)
     count[1] = int(len(sel) > cap)
@@ -90,8 +105,8 @@ def sparta_scatter(vals, idx, count, cap, divisor, dst, layout="rows"):
 def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0, idx=None, vals=None, cap=0,
                          count=None, work=None, skip=None, layout="rows"):
     reps = _rows_view(reps, layout)
-    m = (_np(mask)[:n] != 0) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
-                                                                           skip=_skip_list(skip))
+    m = _mask_bits(mask, n) if mask is not None else osparta.philox_mask(n, seed, iteration, p,
+                                                                         skip=_skip_list(skip))
     r2 = _2d(reps)
     out = osparta.sparse_average(list(_np(r2)[:, :n]), m, divisor)
     for k in range(r2.shape[0]):

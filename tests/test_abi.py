@@ -20,7 +20,7 @@ def test_exports_every_header_symbol():
 
 def test_version_and_struct_layout():
     L = _lib.lib()
-    assert L.ga_abi_version() == 101
+    assert L.ga_abi_version() == 102
     assert L.ga_demo_tensor_bytes() == ctypes.sizeof(_lib.DemoTensor) == 56
 
 
@@ -48,7 +48,12 @@ def test_sparta_gap_table_and_workspace():
     lambda L: L.ga_replica_mean(0, ctypes.c_void_p(64), 2, 4, None, 8, 1.0, ctypes.c_void_p(64), 1, 8, None),
     lambda L: L.ga_diloco_outer(0, ctypes.c_void_p(64), 1, 8, 8, 1.0, ctypes.c_void_p(64), None, 1, 0, 0.7, 0.9,
                                 0.0, 0.0, 1, ctypes.c_void_p(64), 1, 8, None),
-    lambda L: L.ga_sparta_select(0, None, 1, 8, 0, 8, None, 1, 1, 10, None, 0, 8, None, None, None, None, None),
+    lambda L: L.ga_sparta_select(0, None, 1, 8, 0, 8, None, 0, 1, 1, 10, None, 0, 8, None, None, None, None, None),
+    lambda L: L.ga_sparta_select(0, ctypes.c_void_p(64), 1, 8, 0, 8, ctypes.c_void_p(64), 2, 1, 1, 0.5, None, 0, 8,
+                                 ctypes.c_void_p(64), ctypes.c_void_p(64), ctypes.c_void_p(64), ctypes.c_void_p(64),
+                                 None),
+    lambda L: L.ga_sparta_pack_mask(ctypes.c_void_p(64), 100, None, None),
+    lambda L: L.ga_sparta_pack_mask(ctypes.c_void_p(65), 100, ctypes.c_void_p(64), None),
     lambda L: L.ga_demo_encode(0, None, 0, 0, None, None, None, None, None, 1, 8, 0.1, 0.9, 1.0, None, 0, 0, None),
 ])
 def test_invalid_arguments_fail_cleanly(call):

@@ -833,3 +833,82 @@ def test_sparta_average_local_own_groups(K, dtype, ld, p):
     tol = 1e-2 if dtype == torch.bfloat16 else 0
     np.testing.assert_allclose(xs[:, :K].T, np.stack(want), rtol=tol, atol=tol)
     assert (xs[:, K:] == 3.0).all()
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 300_001, 16384 * 3])
+def test_sparta_pack_mask(n):
+    """ga_sparta_pack_mask against oracle.sparta.pack_mask, bit for bit,
+    including the ragged last word (bits past n zero) and non-0/1 mask bytes."""
+    from gym_amd import ops
+    rng = np.random.default_rng(n)
+    m = (rng.random(n) < 0.3).astype(np.uint8) * rng.integers(1, 256, n).astype(np.uint8)
+    mask_t = torch.zeros(n + 64, dtype=torch.uint8, device=DEV)
+    mask_t[:n] = torch.from_numpy(m).to(DEV)
+    mask_t[n:] = 1  # past n: never packed
+    bits = torch.full((ops.sparta_mask_words(n) + 1,), -1, dtype=torch.int64, device=DEV)
+    ops.sparta_pack_mask(mask_t, n, bits)
+    got = bits.cpu().numpy()
+    assert np.array_equal(got[:-1], osparta.pack_mask(m)) and got[-1] == -1
+    assert np.array_equal(osparta.unpack_mask(got[:-1], n), m != 0)
+
+
+@pytest.mark.parametrize("layout,K", [("rows", 3), ("elem", 32)])
+def test_sparta_packed_mask_equals_byte_mask(layout, K):
+    """The packed mask selects exactly what the byte mask selects: select
+    (idx, vals, count) and the fused average, both layouts."""
+    from gym_amd import ops
+    n = 300_001
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    m = rng.random(n) < 0.01
+    mask_t = torch.zeros(n + 15, dtype=torch.uint8, device=DEV)
+    mask_t[:n] = torch.from_numpy(m.astype(np.uint8)).to(DEV)
+    bits = torch.empty(ops.sparta_mask_words(n), dtype=torch.int64, device=DEV)
+    ops.sparta_pack_mask(mask_t, n, bits)
+    mk = (lambda a: t(np.ascontiguousarray(a.T))) if layout == "elem" else t
+    cap = int(m.sum()) + 16
+    outs = []
+    for mk_mask in (mask_t, bits):
+        idx, count, work = _sparta_buffers(n, cap)
+        vals = torch.empty(cap, device=DEV)
+        ops.sparta_select(mk(x), n, cap, idx, vals, count, work, mask=mk_mask, layout=layout)
+        c = int(count[0].item())
+        outs.append((c, idx[:c].cpu().numpy(), host(vals)[:c]))
+        src = mk(x)
+        ops.sparta_average_local(src, n, float(K), mask=mk_mask, layout=layout)
+        got = host(src).T if layout == "elem" else host(src)
+        want = osparta.sparse_average(list(x), m)
+        for k in range(K):
+            assert np.array_equal(got[k], want[k])
+    assert outs[0][0] == outs[1][0] == int(m.sum())
+    assert np.array_equal(outs[0][1], np.flatnonzero(m)) and np.array_equal(outs[1][1], outs[0][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+
+
+def test_sparta_inplace_bernoulli_is_the_reference_draw():
+    """draw_masks' RandomIndexSelector path (view.bernoulli_(cached full(p))
+    into the uint8 arena) gives the reference's torch.bernoulli(torch.full(
+    shape, p)).bool() bits (sparta.py:80-85) and leaves the generator where the
+    reference leaves it, on GPT-2-like shapes, a grad-less tensor skipped."""
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.strategy.sparta import RandomIndexSelector, draw_masks
+    shapes = [(50304, 768), (1024, 768), (768,), (2304, 768), (2304,), (3072, 768), (66, 128), (3, 5, 7), (1,)]
+    L = ArenaLayout(shapes)
+    params = [torch.zeros(s, device=DEV) for s in shapes]
+    sel = RandomIndexSelector(0.005)
+    skip = {3}
+    mask = torch.full((L.n,), 7, dtype=torch.uint8, device=DEV)
+    pfull = []
+    for step in range(2):  # the second step reuses the cached probabilities
+        torch.manual_seed(1234 + step)
+        want = [None if i in skip else sel.get_indices(p, step) for i, p in enumerate(params)]
+        after_ref = torch.rand(8, device=DEV)
+        torch.manual_seed(1234 + step)
+        draw_masks(sel, params, L.views(mask), skip, step, pfull)
+        after = torch.rand(8, device=DEV)
+        assert torch.equal(after, after_ref)
+        for i, v in enumerate(L.views(mask)):
+            if i in skip:
+                assert int(v.sum()) == 0
+            else:
+                assert torch.equal(v.bool(), want[i]), (step, i)
