@@ -333,15 +333,15 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     ops.sparta_average_local = timer.wrap(avg_local)
     it = [0]
     if mask_source == "torch":
-        from gym_amd.strategy.sparta import RandomIndexSelector, draw_masks
-        sel, pfull = RandomIndexSelector(p), []
+        from gym_amd.strategy.sparta import MaskDraw, RandomIndexSelector, draw_masks
+        sel, draw = RandomIndexSelector(p), MaskDraw()
         mask = torch.zeros(layout.n, dtype=torch.uint8, device=dev)
         mviews = layout.views(mask)
         torch.manual_seed(42)
 
     def step():
         if mask_source == "torch":
-            draw_masks(sel, mviews, mviews, set(), it[0], pfull)
+            draw_masks(sel, mviews, mviews, set(), it[0], draw)
             eng(reps, mask=mask, mask_cap=eng.cap)
         else:
             eng(reps, seed=42, iteration=it[0])
@@ -376,7 +376,8 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
                    f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter",
            "mask_source": mask_source}
     if mask_source == "torch":
-        out["mask"] = ("reference per-tensor torch.bernoulli draws (148 launches) into a uint8 arena, in the step" +
+        out["mask"] = ("reference per-tensor torch.bernoulli draws (148 kernels, one HIP graph replay) into a uint8 "
+                       "arena, in the step" +
                        ("" if coll.world == 1 else f"; rank 0's packed to bits and broadcast: "
                         f"{ops.sparta_mask_words(layout.n) * 8 + 8} B instead of {layout.n} B"))
     if queued is not None:

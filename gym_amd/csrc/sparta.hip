@@ -653,6 +653,47 @@ __global__ __launch_bounds__(kSpBlock) void sparta_pack_mask_kernel(const uint8_
     bits[w] = b;
 }
 
+// The reference's mask draw on the GPU, all tensors in one launch: for every
+// drawn tensor i, torch.bernoulli(torch.full(shape_i, p)) on a CUDA/HIP device
+// runs ATen's bernoulli_tensor_cuda_kernel through CUDA_tensor_apply2<.., 4>
+// (block 512, grid ceil(numel / 2048): one pass, no grid-stride reuse below
+// 2^31 blocks): thread t initialises Philox4x32-10 with (seed, subsequence t,
+// offset O_i) -- counter {O_i/4 lo, O_i/4 hi, t lo, t hi}, key seed (O_i % 4 ==
+// 0) -- takes one uniform4 (u = 2^-32 + w * 2^-32 per 32-bit word w, float)
+// and selects element 4t + j iff u_j <= p (float).  O_i = O_0 + i * step, the
+// generator offset torch hands out per bernoulli_ call.  One lane per
+// 4-element group; a workgroup stays inside one tensor (table rows: arena
+// offset, numel, first workgroup), so the lookup is a uniform binary search.
+__global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const int64_t* __restrict__ tab, int ntens,
+                                                                         float p, uint2 key, uint64_t off0,
+                                                                         uint64_t step, uint8_t* __restrict__ mask) {
+    const int b = (int)blockIdx.x;
+    int lo = 0, hi = ntens - 1;
+    while (lo < hi) {  // last row whose first workgroup <= b
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[3 * mid + 2] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t base = tab[3 * lo], numel = tab[3 * lo + 1];
+    const uint64_t t = (uint64_t)(b - tab[3 * lo + 2]) * kSpBlock + threadIdx.x;
+    const int64_t e0 = (int64_t)t * 4;
+    if (e0 >= numel) return;
+    const uint64_t ctr = (off0 + (uint64_t)lo * step) >> 2;
+    const uint4 w = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
+                                  key);
+    const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    uint8_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (inv + (float)ws[j] * inv) <= p ? 1 : 0;
+    uint8_t* m = mask + base + e0;
+    if (e0 + 4 <= numel) {
+        *reinterpret_cast<uchar4*>(m) = make_uchar4(v[0], v[1], v[2], v[3]);
+    } else {
+        for (int j = 0; e0 + j < numel; ++j) m[j] = v[j];
+    }
+}
+
 static int64_t sparta_tiles(int64_t n) { return ceil_div(n, kSpTile); }
 
 static Rep make_rep(int64_t ld, int layout) {
@@ -797,6 +838,20 @@ extern "C" GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64
     hipLaunchKernelGGL(sparta_pack_mask_kernel, dim3((unsigned)ceil_div(words, (int64_t)kSpBlock)), dim3(kSpBlock), 0,
                        stream, mask, n, bits);
     return check_launch("ga_sparta_pack_mask");
+}
+
+extern "C" GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
+                                                uint64_t seed, uint64_t offset0, uint64_t offset_step, uint8_t* mask,
+                                                hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(ntens >= 0 && nblocks >= 0 && nblocks < (int64_t)INT32_MAX, "ga_sparta_torch_bernoulli: bad sizes");
+    GA_REQUIRE(p >= 0.f && p <= 1.f, "ga_sparta_torch_bernoulli: p=%g outside [0, 1]", (double)p);
+    GA_REQUIRE(offset0 % 4 == 0 && offset_step % 4 == 0, "ga_sparta_torch_bernoulli: offsets must be multiples of 4");
+    if (ntens == 0 || nblocks == 0) return GA_OK;
+    GA_REQUIRE(table && mask && ((uintptr_t)mask % 4) == 0, "ga_sparta_torch_bernoulli: null table/mask or mask alignment");
+    hipLaunchKernelGGL(sparta_torch_bernoulli_kernel, dim3((unsigned)nblocks), dim3(kSpBlock), 0, stream, table,
+                       (int)ntens, p, make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)), offset0, offset_step, mask);
+    return check_launch("ga_sparta_torch_bernoulli");
 }
 
 extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32_t* idx, const int64_t* count,

@@ -130,6 +130,37 @@ def sparta_pack_mask(mask, n, bits):
     check(lib().ga_sparta_pack_mask(_p(mask), int(n), _p(bits), _stream()), "ga_sparta_pack_mask")
 
 
+TORCH_BERNOULLI_BLOCK = 256  # lanes per workgroup of ga_sparta_torch_bernoulli (4 elements per lane)
+
+
+def sparta_bernoulli_table(offsets, numels, device):
+    """(int64 [T, 3] device table, workgroups) for ga_sparta_torch_bernoulli:
+    per drawn tensor its arena offset, numel and first workgroup."""
+    rows, b = [], 0
+    per = 4 * TORCH_BERNOULLI_BLOCK
+    for o, n in zip(offsets, numels):
+        if o % 4:
+            raise ValueError("sparta_bernoulli_table: arena offsets must be multiples of 4")
+        rows.append((int(o), int(n), b))
+        b += (int(n) + per - 1) // per
+    t = torch.tensor(rows, dtype=torch.int64, device=device).view(-1, 3)
+    return t, b
+
+
+def sparta_torch_bernoulli(table, nblocks, p, seed, offset0, offset_step, mask):
+    """mask[arena offset of tensor i + e] <- torch.bernoulli(torch.full(shape_i,
+    p)) element e as ATen's HIP kernel draws it with generator (seed, offset0 +
+    i * offset_step); every drawn tensor in one launch."""
+    _gpu(table, mask)
+    if mask.dtype != torch.uint8 or not mask.is_contiguous():
+        raise ValueError("sparta_torch_bernoulli: mask must be a contiguous uint8 arena")
+    if table.dtype != torch.int64 or table.dim() != 2 or table.shape[1] != 3 or not table.is_contiguous():
+        raise ValueError("sparta_torch_bernoulli: table must be a contiguous int64 [T, 3] tensor")
+    check(lib().ga_sparta_torch_bernoulli(_p(table), int(table.shape[0]), int(nblocks), float(p),
+                                          int(seed) & (2**64 - 1), int(offset0), int(offset_step), _p(mask),
+                                          _stream()), "ga_sparta_torch_bernoulli")
+
+
 def _mask_arg(mask, n, who):
     """(mask, format code) of a SPARTA mask: uint8/bool per element, or int64
     packed words (sparta_pack_mask)."""

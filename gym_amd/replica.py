@@ -33,7 +33,7 @@ from .fused_optim import ArenaAdam, fusable
 from .strategy.demo import DeMoStrategy
 from .strategy.diloco import DiLoCoStrategy, fused_sgd_hparams
 from .strategy.federated_averaging import FedAvgStrategy
-from .strategy.sparta import RandomIndexSelector, SPARTAStrategy, draw_masks
+from .strategy.sparta import MaskDraw, RandomIndexSelector, SPARTAStrategy, draw_masks
 from .strategy.strategy import SimpleReduceStrategy, clip_arena_grad_norm_
 
 
@@ -136,7 +136,7 @@ class ReplicaRunner:
                     self.seed = int(t.item())
                 else:
                     self.mask = torch.zeros(ld, dtype=torch.uint8, device=dev)
-                    self.pfull = []
+                    self.draw = MaskDraw()
                 self.iteration = 0
         # the strategy's LR schedule on every optimizer (strategy.py:75-112)
         for o in (self.optim.opts if isinstance(self.optim, _PerNodeOptim) else [self.optim]):
@@ -209,7 +209,7 @@ class ReplicaRunner:
         process's and broadcasts it to the others."""
         a0 = self.ra.arenas[0]
         draw_masks(self.s.index_selector, a0.params, self.ra.layout.views(self.mask), set(self._grad_less()),
-                   self.iteration, self.pfull)
+                   self.iteration, self.draw)
         return self.mask
 
     def _inner(self):

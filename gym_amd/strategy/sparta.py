@@ -37,6 +37,7 @@ from typing import Optional, Union
 
 import torch
 
+from .. import ops
 from ..engine import Sparta
 from .communicate_optimize_strategy import CommunicateOptimizeStrategy, CommunicationModule
 from .optim import OptimSpec
@@ -62,30 +63,103 @@ class RandomIndexSelector(IndexSelector):
         return torch.bernoulli(torch.full(param.shape, self.p, device=param.device)).bool()
 
 
-def draw_masks(selector, params, views, skip, iteration, pfull):
+class MaskDraw:
+    """State of draw_masks for one mask arena: the fused kernel's tensor table;
+    for the per-tensor torch path the cached probability tensors and the HIP
+    graph of the draw sequence."""
+
+    fused = True       # one ga_sparta_torch_bernoulli launch for every tensor (GPU)
+    use_graphs = True  # otherwise: the per-tensor torch draws, as one HIP graph replay
+    offset_step = 12   # generator offset per bernoulli_ call (philox_cuda_state(10), rounded up to 4)
+
+    def __init__(self):
+        self.pfull = []
+        self.key = None
+        self.graph = None
+        self.calls = 0
+        self.table = None
+
+
+def draw_masks(selector, params, views, skip, iteration, state):
     """Every tensor's selector mask into its view of a uint8 mask arena, in
     parameter order (sparta.py:28-33); tensors in `skip` stay 0.
 
-    RandomIndexSelector: `view.bernoulli_(P)` with P = the cached
+    RandomIndexSelector on a GPU: one ga_sparta_torch_bernoulli launch draws
+    every tensor's mask exactly as the per-tensor torch.bernoulli calls would
+    (same bits, generator advanced by the same amount; _draw_fused).  With
+    MaskDraw.fused off: `view.bernoulli_(P)` with P = the cached
     torch.full(shape, p) of the tensor -- the same bernoulli kernel on the same
     probabilities as the reference's torch.bernoulli(torch.full(shape, p))
     (so the same bits and the same generator offsets), written straight into
-    the arena: no per-step fill of 4 B/element, no float mask, no copy.
-    pfull: the per-tensor cache (a list, filled here).  Other selectors: their
-    get_indices, copied in."""
+    the arena: no per-step fill of 4 B/element, no float mask, no copy.  The
+    sequence is launch-bound (one small kernel per tensor), so from its second
+    call on a GPU it runs as one captured HIP graph: a replay reads the
+    generator's seed/offset at replay time and advances it by the captured
+    total, i.e. draws exactly what the eager sequence would.  Other
+    selectors: their get_indices, copied in (eager)."""
     fast = type(selector) is RandomIndexSelector
-    if fast and len(pfull) != len(params):
-        pfull[:] = [None] * len(params)
-    for i, (p, v) in enumerate(zip(params, views)):
-        if i in skip:
-            v.zero_()
-        elif fast:
-            P = pfull[i]
-            if P is None or P.shape != p.shape or P.device != p.device:
-                P = pfull[i] = torch.full(p.shape, selector.p, device=p.device)
-            v.bernoulli_(P)
-        else:
-            v.copy_(selector.get_indices(p, iteration))
+    if not fast:
+        for i, (p, v) in enumerate(zip(params, views)):
+            if i in skip:
+                v.zero_()
+            else:
+                v.copy_(selector.get_indices(p, iteration))
+        return
+    key = (tuple(v.data_ptr() for v in views), tuple(tuple(p.shape) for p in params), frozenset(skip),
+           float(selector.p), str(params[0].device) if params else "")
+    if key != state.key:
+        state.key, state.graph, state.calls, state.table = key, None, 0, None
+        state.pfull = [None] * len(params)
+
+    def body():
+        for i, (p, v) in enumerate(zip(params, views)):
+            if i in skip:
+                v.zero_()
+            else:
+                v.bernoulli_(state.pfull[i])
+
+    on_gpu = bool(params) and params[0].device.type == "cuda"
+    if on_gpu and MaskDraw.fused:
+        _draw_fused(selector, params, views, skip, state)
+        state.calls += 1
+        return
+    for i, p in enumerate(params):
+        if i not in skip and state.pfull[i] is None:
+            state.pfull[i] = torch.full(p.shape, selector.p, device=p.device)
+    if on_gpu and MaskDraw.use_graphs and state.graph is None and state.calls >= 1:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        state.graph = g
+    if state.graph is not None:
+        state.graph.replay()
+    else:
+        body()
+    state.calls += 1
+
+
+def _draw_fused(selector, params, views, skip, state):
+    """Every drawn tensor's torch.bernoulli(torch.full(shape, p)) in ONE launch
+    (ga_sparta_torch_bernoulli: ATen's HIP kernel for it restated, bit for
+    bit), with the default generator of the device read and advanced exactly
+    as the per-tensor calls would (offset_step per drawn tensor)."""
+    if state.table is None:
+        base = views[0]._base if views[0]._base is not None else views[0]
+        if base.dtype != torch.uint8 or not base.is_contiguous():
+            raise ValueError("draw_masks: views must be views of one contiguous uint8 mask arena")
+        drawn = [i for i in range(len(params)) if i not in skip]
+        offs = [views[i].storage_offset() - base.storage_offset() for i in drawn]
+        state.table = ops.sparta_bernoulli_table(offs, [views[i].numel() for i in drawn], base.device)
+        state.base, state.ndrawn = base, len(drawn)
+    for i in skip:
+        views[i].zero_()
+    table, nblocks = state.table
+    dev = state.base.device
+    gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+    off0 = gen.get_offset()
+    ops.sparta_torch_bernoulli(table, nblocks, float(selector.p), gen.initial_seed(), off0, MaskDraw.offset_step,
+                               state.base)
+    gen.set_offset(off0 + MaskDraw.offset_step * state.ndrawn)
 
 
 class ShuffledSequentialIndexSelector(IndexSelector):
@@ -151,7 +225,7 @@ class SparseCommunicator(CommunicationModule):
         self._mask = None
         self._skip_key = None
         self._skip = None
-        self._pfull = []
+        self._draw = MaskDraw()
 
     def _init_node(self, model, rank, num_nodes):
         pass
@@ -200,7 +274,7 @@ class SparseCommunicator(CommunicationModule):
         if self._mask is None:
             self._mask = torch.zeros(a.n, dtype=torch.uint8, device=a.device)
         skip = {i for i, p in enumerate(a.params) if not p.requires_grad or p.grad is None}
-        draw_masks(self.index_selector, a.params, a.layout.views(self._mask), skip, self.iteration, self._pfull)
+        draw_masks(self.index_selector, a.params, a.layout.views(self._mask), skip, self.iteration, self._draw)
         return self._mask
 
     def _mask_cap(self):

@@ -139,6 +139,21 @@ GA_API void ga_sparta_gap_table(double p, uint64_t* table);
 GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, hipStream_t stream);
 
 /*
+ * The reference's per-tensor mask draw, RandomIndexSelector.get_indices =
+ * torch.bernoulli(torch.full(shape, p, device=cuda)) (sparta.py:80-85), for
+ * every drawn tensor in one launch, bit-identical to ATen's HIP kernel for it:
+ * tensor i (table row i = {arena offset (a multiple of 4), numel, first
+ * workgroup}, workgroups of 256 lanes, each lane one 4-element group,
+ * nblocks in total) uses generator offset offset0 + i * offset_step; element
+ * 4t + j of the tensor is selected iff the j-th uniform of Philox4x32-10
+ * (key seed, counter {offset/4, t}) is <= p.  mask[offset + e] <- 0/1.
+ * The caller advances the torch generator by ntens * offset_step.
+ */
+GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
+                                     uint64_t seed, uint64_t offset0, uint64_t offset_step, uint8_t* mask,
+                                     hipStream_t stream);
+
+/*
  * Select the SPARTA index set over an arena of n elements and gather the
  * selected values summed over the K local replicas (replica set in `layout`,
  * GA_LAYOUT_*).

@@ -17,6 +17,9 @@ geometric gaps between selected elements of each 64-element group (one
 Bernoulli(p) draw per element in distribution; `philox_mask`).
 `philox4x32_10` restates that generator; it is pinned by the Random123
 known-answer vectors in tests/test_oracle_golden.py.
+`torch_gpu_bernoulli` restates the reference draw as torch runs it on a GPU
+(ATen's HIP bernoulli kernel over rocrand Philox4x32-10; third-party code, no
+reference source), pinned on the GPU box against torch.bernoulli itself.
 """
 import math
 
@@ -183,3 +186,25 @@ def unpack_mask(words, n):
     """Inverse of pack_mask: the n-element bool mask."""
     b = np.unpackbits(np.asarray(words, dtype="<i8").view(np.uint8), bitorder="little")
     return b[:n].astype(bool)
+
+
+def torch_gpu_bernoulli(numel, p, seed, offset):
+    """torch.bernoulli(torch.full((numel,), p, device=cuda)) as ATen's HIP
+    kernel draws it (bernoulli_tensor_cuda_kernel via CUDA_tensor_apply2<.., 4>,
+    hiprand/rocrand Philox4x32-10): thread t = element // 4 initialises the
+    generator with (seed, subsequence t, offset) -- counter {offset/4, t}, key
+    seed -- and element 4t + j is selected iff float32(w_j) * 2^-32 + 2^-32 <=
+    float32(p) (float32 arithmetic), w_j the j-th word of its first Philox call.
+    Third-party restatement (torch 2.10 / ROCm rocrand, no reference source):
+    pinned by tests/test_gpu_kernels.py against torch.bernoulli on the GPU."""
+    assert offset % 4 == 0
+    T = -(-int(numel) // 4)
+    t = np.arange(T, dtype=np.uint64)
+    q = np.uint64(offset // 4)
+    ctr = np.stack([np.full(T, q & MASK32), np.full(T, q >> np.uint64(32)), t & MASK32, t >> np.uint64(32)],
+                   axis=-1).astype(np.uint32)
+    key = np.array([seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF], dtype=np.uint32)
+    w = philox4x32_10(ctr, key).reshape(-1)[:numel]
+    inv = np.float32(2.0 ** -32)
+    u = w.astype(np.float32) * inv + inv
+    return u <= np.float32(p)

@@ -885,30 +885,61 @@ def test_sparta_packed_mask_equals_byte_mask(layout, K):
     assert np.array_equal(outs[0][2], outs[1][2])
 
 
-def test_sparta_inplace_bernoulli_is_the_reference_draw():
+@pytest.mark.parametrize("mode", ["fused", "graph", "eager"])
+def test_sparta_inplace_bernoulli_is_the_reference_draw(mode):
     """draw_masks' RandomIndexSelector path (view.bernoulli_(cached full(p))
-    into the uint8 arena) gives the reference's torch.bernoulli(torch.full(
-    shape, p)).bool() bits (sparta.py:80-85) and leaves the generator where the
-    reference leaves it, on GPT-2-like shapes, a grad-less tensor skipped."""
+    into the uint8 arena; from the second call one HIP graph replay of the
+    whole sequence) gives the reference's torch.bernoulli(torch.full(shape,
+    p)).bool() bits (sparta.py:80-85) and leaves the generator where the
+    reference leaves it, step after step, on GPT-2-like shapes with a
+    grad-less tensor skipped."""
     from gym_amd.arena import ArenaLayout
-    from gym_amd.strategy.sparta import RandomIndexSelector, draw_masks
+    from gym_amd.strategy.sparta import MaskDraw, RandomIndexSelector, draw_masks
     shapes = [(50304, 768), (1024, 768), (768,), (2304, 768), (2304,), (3072, 768), (66, 128), (3, 5, 7), (1,)]
     L = ArenaLayout(shapes)
     params = [torch.zeros(s, device=DEV) for s in shapes]
     sel = RandomIndexSelector(0.005)
     skip = {3}
     mask = torch.full((L.n,), 7, dtype=torch.uint8, device=DEV)
-    pfull = []
-    for step in range(2):  # the second step reuses the cached probabilities
-        torch.manual_seed(1234 + step)
+    state = MaskDraw()
+    saved = (MaskDraw.fused, MaskDraw.use_graphs)
+    MaskDraw.fused, MaskDraw.use_graphs = mode == "fused", mode == "graph"
+    torch.manual_seed(1234)
+    for step in range(4):  # eager, capture + replay, replay, replay
+        gen = torch.cuda.get_rng_state()
         want = [None if i in skip else sel.get_indices(p, step) for i, p in enumerate(params)]
-        after_ref = torch.rand(8, device=DEV)
-        torch.manual_seed(1234 + step)
-        draw_masks(sel, params, L.views(mask), skip, step, pfull)
-        after = torch.rand(8, device=DEV)
-        assert torch.equal(after, after_ref)
+        after_ref = torch.cuda.get_rng_state()
+        torch.cuda.set_rng_state(gen)
+        mask.fill_(7)
+        draw_masks(sel, params, L.views(mask), skip, step, state)
+        assert torch.equal(torch.cuda.get_rng_state(), after_ref), step
         for i, v in enumerate(L.views(mask)):
             if i in skip:
                 assert int(v.sum()) == 0
             else:
                 assert torch.equal(v.bool(), want[i]), (step, i)
+        torch.rand(5, device=DEV)  # other consumers of the generator between steps
+    MaskDraw.fused, MaskDraw.use_graphs = saved
+    assert (state.graph is not None) == (mode == "graph")
+
+
+@pytest.mark.parametrize("numel,p", [(1, 0.5), (7, 0.3), (4096 * 3 + 2, 0.005), (2_000_003, 0.005), (100_000, 0.9)])
+def test_torch_gpu_bernoulli_oracle_and_kernel(numel, p):
+    """oracle.sparta.torch_gpu_bernoulli restates ATen's HIP bernoulli kernel
+    (pinned here against torch.bernoulli(torch.full(...)) on this GPU), and
+    ga_sparta_torch_bernoulli equals both, at a ragged numel and a tensor that
+    starts inside the mask arena."""
+    from gym_amd import ops
+    gen = torch.cuda.default_generators[0]
+    torch.manual_seed(777)
+    torch.rand(3, device=DEV)  # a non-zero starting offset
+    seed, off = gen.initial_seed(), gen.get_offset()
+    want = torch.bernoulli(torch.full((numel,), p, device=DEV)).bool().cpu().numpy()
+    assert gen.get_offset() == off + 12  # the offset step draw_masks assumes
+    assert np.array_equal(osparta.torch_gpu_bernoulli(numel, p, seed, off), want)
+    mask = torch.full((64 + numel + 64,), 9, dtype=torch.uint8, device=DEV)
+    table, nb = ops.sparta_bernoulli_table([64], [numel], DEV)
+    ops.sparta_torch_bernoulli(table, nb, p, seed, off, 12, mask)
+    got = mask.cpu().numpy()
+    assert np.array_equal(got[64:64 + numel] != 0, want) and set(np.unique(got[64:64 + numel])) <= {0, 1}
+    assert (got[:64] == 9).all() and (got[64 + numel:] == 9).all()
