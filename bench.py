@@ -337,12 +337,13 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
         sel, draw = RandomIndexSelector(p), MaskDraw()
         mask = torch.zeros(layout.n, dtype=torch.uint8, device=dev)
         mviews = layout.views(mask)
+        mbits = torch.zeros(ops.sparta_mask_words(layout.n), dtype=torch.int64, device=dev)
         torch.manual_seed(42)
 
     def step():
         if mask_source == "torch":
-            draw_masks(sel, mviews, mviews, set(), it[0], draw)
-            eng(reps, mask=mask, mask_cap=eng.cap)
+            packed = draw_masks(sel, mviews, mviews, set(), it[0], draw, bits=mbits)
+            eng(reps, mask=mask if packed is None else packed, mask_cap=eng.cap)
         else:
             eng(reps, seed=42, iteration=it[0])
         it[0] += 1
@@ -376,10 +377,10 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
                    f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter",
            "mask_source": mask_source}
     if mask_source == "torch":
-        out["mask"] = ("reference per-tensor torch.bernoulli draws (148 kernels, one HIP graph replay) into a uint8 "
-                       "arena, in the step" +
-                       ("" if coll.world == 1 else f"; rank 0's packed to bits and broadcast: "
-                        f"{ops.sparta_mask_words(layout.n) * 8 + 8} B instead of {layout.n} B"))
+        out["mask"] = ("the reference's per-tensor torch.bernoulli draws, bit-identical, as one "
+                       "ga_sparta_torch_bernoulli launch writing the packed mask, in the step" +
+                       ("" if coll.world == 1 else f"; rank 0's broadcast: "
+                        f"{ops.sparta_mask_words(layout.n) * 8} B instead of the reference's {layout.n} B"))
     if queued is not None:
         out["kernel_ms"] = round(queued, 4)
         out["kernel_alg_GBps"] = round(alg / (queued * 1e-3) / 1e9, 1)

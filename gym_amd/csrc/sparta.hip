@@ -664,9 +664,10 @@ __global__ __launch_bounds__(kSpBlock) void sparta_pack_mask_kernel(const uint8_
 // generator offset torch hands out per bernoulli_ call.  One lane per
 // 4-element group; a workgroup stays inside one tensor (table rows: arena
 // offset, numel, first workgroup), so the lookup is a uniform binary search.
+template <bool BITS>
 __global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const int64_t* __restrict__ tab, int ntens,
                                                                          float p, uint2 key, uint64_t off0,
-                                                                         uint64_t step, uint8_t* __restrict__ mask) {
+                                                                         uint64_t step, void* __restrict__ mask) {
     const int b = (int)blockIdx.x;
     int lo = 0, hi = ntens - 1;
     while (lo < hi) {  // last row whose first workgroup <= b
@@ -677,20 +678,36 @@ __global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const 
     const int64_t base = tab[3 * lo], numel = tab[3 * lo + 1];
     const uint64_t t = (uint64_t)(b - tab[3 * lo + 2]) * kSpBlock + threadIdx.x;
     const int64_t e0 = (int64_t)t * 4;
-    if (e0 >= numel) return;
-    const uint64_t ctr = (off0 + (uint64_t)lo * step) >> 2;
-    const uint4 w = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
-                                  key);
-    const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
-    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-    uint8_t v[4];
+    uint32_t v[4] = {0u, 0u, 0u, 0u};
+    if (e0 < numel) {
+        const uint64_t ctr = (off0 + (uint64_t)lo * step) >> 2;
+        const uint4 w = philox4x32_10(
+            make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)), key);
+        const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (inv + (float)ws[j] * inv) <= p ? 1 : 0;
-    uint8_t* m = mask + base + e0;
-    if (e0 + 4 <= numel) {
-        *reinterpret_cast<uchar4*>(m) = make_uchar4(v[0], v[1], v[2], v[3]);
+        for (int j = 0; j < 4; ++j) v[j] = (e0 + j < numel && (inv + (float)ws[j] * inv) <= p) ? 1u : 0u;
+    }
+    if constexpr (BITS) {
+        // 16 consecutive lanes = one 64-element word (t % 16 == 0 at lane 16q; base % 64 == 0)
+        const int sh = 4 * (int)(threadIdx.x & 15);
+        const uint32_t nib = v[0] | (v[1] << 1) | (v[2] << 2) | (v[3] << 3);
+        uint32_t lo32 = sh < 32 ? nib << sh : 0u, hi32 = sh >= 32 ? nib << (sh - 32) : 0u;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            lo32 |= (uint32_t)__shfl_xor((int)lo32, d, 64);
+            hi32 |= (uint32_t)__shfl_xor((int)hi32, d, 64);
+        }
+        if ((threadIdx.x & 15) == 0 && e0 < numel)
+            reinterpret_cast<uint64_t*>(mask)[(base + e0) >> 6] = ((uint64_t)hi32 << 32) | lo32;
     } else {
-        for (int j = 0; e0 + j < numel; ++j) m[j] = v[j];
+        if (e0 >= numel) return;
+        uint8_t* m = reinterpret_cast<uint8_t*>(mask) + base + e0;
+        if (e0 + 4 <= numel) {
+            *reinterpret_cast<uchar4*>(m) = make_uchar4(v[0], v[1], v[2], v[3]);
+        } else {
+            for (int j = 0; e0 + j < numel; ++j) m[j] = (uint8_t)v[j];
+        }
     }
 }
 
@@ -841,16 +858,22 @@ extern "C" GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64
 }
 
 extern "C" GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
-                                                uint64_t seed, uint64_t offset0, uint64_t offset_step, uint8_t* mask,
-                                                hipStream_t stream) {
+                                                uint64_t seed, uint64_t offset0, uint64_t offset_step, void* mask,
+                                                int mask_format, hipStream_t stream) {
     clear_error();
+    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS,
+               "ga_sparta_torch_bernoulli: bad mask_format %d", mask_format);
     GA_REQUIRE(ntens >= 0 && nblocks >= 0 && nblocks < (int64_t)INT32_MAX, "ga_sparta_torch_bernoulli: bad sizes");
     GA_REQUIRE(p >= 0.f && p <= 1.f, "ga_sparta_torch_bernoulli: p=%g outside [0, 1]", (double)p);
     GA_REQUIRE(offset0 % 4 == 0 && offset_step % 4 == 0, "ga_sparta_torch_bernoulli: offsets must be multiples of 4");
     if (ntens == 0 || nblocks == 0) return GA_OK;
-    GA_REQUIRE(table && mask && ((uintptr_t)mask % 4) == 0, "ga_sparta_torch_bernoulli: null table/mask or mask alignment");
-    hipLaunchKernelGGL(sparta_torch_bernoulli_kernel, dim3((unsigned)nblocks), dim3(kSpBlock), 0, stream, table,
-                       (int)ntens, p, make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)), offset0, offset_step, mask);
+    GA_REQUIRE(table && mask && ((uintptr_t)mask % 8) == 0, "ga_sparta_torch_bernoulli: null table/mask or mask alignment");
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kSpBlock), 0, stream, table, (int)ntens, p,
+                           make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)), offset0, offset_step, mask);
+    };
+    if (mask_format == GA_MASK_BITS) go(sparta_torch_bernoulli_kernel<true>);
+    else go(sparta_torch_bernoulli_kernel<false>);
     return check_launch("ga_sparta_torch_bernoulli");
 }
 

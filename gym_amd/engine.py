@@ -276,7 +276,7 @@ class Sparta:
 
     def __call__(self, reps, seed=0, iteration=0, mask=None, skip=None, mask_cap=None):
         """mask: this process's uint8/bool mask arena (the reference selector's
-        draws) or None for the Philox stream.  With an exchange, rank 0's mask
+        draws), or its packed int64 words, or None for the Philox stream.  With an exchange, rank 0's mask
         wins (sparta.py:32-37): it is packed to one bit per element and
         broadcast (n/8 bytes; every rank's own draw is overwritten).
         mask_cap: a bound on the selected count that holds on every rank (e.g.
@@ -285,7 +285,12 @@ class Sparta:
         count is read back (any selector)."""
         n = self.n
         cnt = None
-        if mask is not None and self.coll.exchange:
+        if mask is not None and mask.dtype == torch.int64:  # already packed (the fused reference draw)
+            if mask_cap is None:
+                raise ValueError("Sparta: a packed mask needs mask_cap")
+            if self.coll.exchange:
+                self.coll.broadcast_(mask[:ops.sparta_mask_words(n)], 0)
+        elif mask is not None and self.coll.exchange:
             words = ops.sparta_mask_words(n)
             if self.bits is None:  # the packed words + rank 0's selected count in the last word
                 self.bits = torch.empty(words + 1, dtype=torch.int64, device=self.device)

@@ -135,12 +135,13 @@ TORCH_BERNOULLI_BLOCK = 256  # lanes per workgroup of ga_sparta_torch_bernoulli 
 
 def sparta_bernoulli_table(offsets, numels, device):
     """(int64 [T, 3] device table, workgroups) for ga_sparta_torch_bernoulli:
-    per drawn tensor its arena offset, numel and first workgroup."""
+    per drawn tensor its arena offset (a multiple of 64: the packed form's
+    words never straddle tensors), numel and first workgroup."""
     rows, b = [], 0
     per = 4 * TORCH_BERNOULLI_BLOCK
     for o, n in zip(offsets, numels):
-        if o % 4:
-            raise ValueError("sparta_bernoulli_table: arena offsets must be multiples of 4")
+        if o % 64:
+            raise ValueError("sparta_bernoulli_table: arena offsets must be multiples of 64")
         rows.append((int(o), int(n), b))
         b += (int(n) + per - 1) // per
     t = torch.tensor(rows, dtype=torch.int64, device=device).view(-1, 3)
@@ -148,16 +149,18 @@ def sparta_bernoulli_table(offsets, numels, device):
 
 
 def sparta_torch_bernoulli(table, nblocks, p, seed, offset0, offset_step, mask):
-    """mask[arena offset of tensor i + e] <- torch.bernoulli(torch.full(shape_i,
-    p)) element e as ATen's HIP kernel draws it with generator (seed, offset0 +
-    i * offset_step); every drawn tensor in one launch."""
+    """Element e of drawn tensor i <- torch.bernoulli(torch.full(shape_i, p))
+    element e as ATen's HIP kernel draws it with generator (seed, offset0 + i *
+    offset_step); every drawn tensor in one launch.  mask: the uint8 arena
+    (byte at arena offset + e) or int64 packed words (bit arena offset + e)."""
     _gpu(table, mask)
-    if mask.dtype != torch.uint8 or not mask.is_contiguous():
-        raise ValueError("sparta_torch_bernoulli: mask must be a contiguous uint8 arena")
+    if mask.dtype not in (torch.uint8, torch.int64) or not mask.is_contiguous():
+        raise ValueError("sparta_torch_bernoulli: mask must be a contiguous uint8 arena or int64 packed words")
+    fmt = _lib.GA_MASK_BITS if mask.dtype == torch.int64 else _lib.GA_MASK_BYTES
     if table.dtype != torch.int64 or table.dim() != 2 or table.shape[1] != 3 or not table.is_contiguous():
         raise ValueError("sparta_torch_bernoulli: table must be a contiguous int64 [T, 3] tensor")
     check(lib().ga_sparta_torch_bernoulli(_p(table), int(table.shape[0]), int(nblocks), float(p),
-                                          int(seed) & (2**64 - 1), int(offset0), int(offset_step), _p(mask),
+                                          int(seed) & (2**64 - 1), int(offset0), int(offset_step), _p(mask), fmt,
                                           _stream()), "ga_sparta_torch_bernoulli")
 
 

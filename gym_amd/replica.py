@@ -136,6 +136,7 @@ class ReplicaRunner:
                     self.seed = int(t.item())
                 else:
                     self.mask = torch.zeros(ld, dtype=torch.uint8, device=dev)
+                    self.bits = torch.zeros(ops.sparta_mask_words(ld), dtype=torch.int64, device=dev)
                     self.draw = MaskDraw()
                 self.iteration = 0
         # the strategy's LR schedule on every optimizer (strategy.py:75-112)
@@ -208,9 +209,9 @@ class ReplicaRunner:
         sparta.py:32-37) as one uint8 arena; the engine packs the first
         process's and broadcasts it to the others."""
         a0 = self.ra.arenas[0]
-        draw_masks(self.s.index_selector, a0.params, self.ra.layout.views(self.mask), set(self._grad_less()),
-                   self.iteration, self.draw)
-        return self.mask
+        packed = draw_masks(self.s.index_selector, a0.params, self.ra.layout.views(self.mask), set(self._grad_less()),
+                            self.iteration, self.draw, bits=self.bits)
+        return self.mask if packed is None else packed
 
     def _inner(self):
         if isinstance(self.optim, ArenaAdam):

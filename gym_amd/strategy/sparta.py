@@ -80,9 +80,12 @@ class MaskDraw:
         self.table = None
 
 
-def draw_masks(selector, params, views, skip, iteration, state):
+def draw_masks(selector, params, views, skip, iteration, state, bits=None):
     """Every tensor's selector mask into its view of a uint8 mask arena, in
-    parameter order (sparta.py:28-33); tensors in `skip` stay 0.
+    parameter order (sparta.py:28-33); tensors in `skip` stay 0.  Returns the
+    mask to select with: `bits` (int64 packed words of the same arena,
+    ga_sparta_pack_mask layout) when the fused GPU draw wrote them there
+    instead of the bytes, else None (the uint8 arena holds the masks).
 
     RandomIndexSelector on a GPU: one ga_sparta_torch_bernoulli launch draws
     every tensor's mask exactly as the per-tensor torch.bernoulli calls would
@@ -120,9 +123,9 @@ def draw_masks(selector, params, views, skip, iteration, state):
 
     on_gpu = bool(params) and params[0].device.type == "cuda"
     if on_gpu and MaskDraw.fused:
-        _draw_fused(selector, params, views, skip, state)
+        out = _draw_fused(selector, params, views, skip, state, bits)
         state.calls += 1
-        return
+        return out
     for i, p in enumerate(params):
         if i not in skip and state.pfull[i] is None:
             state.pfull[i] = torch.full(p.shape, selector.p, device=p.device)
@@ -138,11 +141,13 @@ def draw_masks(selector, params, views, skip, iteration, state):
     state.calls += 1
 
 
-def _draw_fused(selector, params, views, skip, state):
+def _draw_fused(selector, params, views, skip, state, bits=None):
     """Every drawn tensor's torch.bernoulli(torch.full(shape, p)) in ONE launch
     (ga_sparta_torch_bernoulli: ATen's HIP kernel for it restated, bit for
     bit), with the default generator of the device read and advanced exactly
-    as the per-tensor calls would (offset_step per drawn tensor)."""
+    as the per-tensor calls would (offset_step per drawn tensor).  With `bits`
+    (int64 words covering the arena, the arena's trailing words zero) the
+    masks are written packed, one bit per element, and `bits` is returned."""
     if state.table is None:
         base = views[0]._base if views[0]._base is not None else views[0]
         if base.dtype != torch.uint8 or not base.is_contiguous():
@@ -151,15 +156,27 @@ def _draw_fused(selector, params, views, skip, state):
         offs = [views[i].storage_offset() - base.storage_offset() for i in drawn]
         state.table = ops.sparta_bernoulli_table(offs, [views[i].numel() for i in drawn], base.device)
         state.base, state.ndrawn = base, len(drawn)
-    for i in skip:
-        views[i].zero_()
+        # packed words of the skipped tensors (their offsets are multiples of 64)
+        state.skip_words = [((views[i].storage_offset() - base.storage_offset()) // 64,
+                             -(-(views[i].storage_offset() - base.storage_offset() + views[i].numel()) // 64))
+                            for i in sorted(skip)]
+    out = state.base
+    if bits is not None:
+        if bits.dtype != torch.int64 or bits.numel() < ops.sparta_mask_words(state.base.numel()):
+            raise ValueError("draw_masks: bits must be int64 words covering the mask arena")
+        for a, b in state.skip_words:
+            bits[a:b].zero_()
+        out = bits
+    else:
+        for i in skip:
+            views[i].zero_()
     table, nblocks = state.table
     dev = state.base.device
     gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
     off0 = gen.get_offset()
-    ops.sparta_torch_bernoulli(table, nblocks, float(selector.p), gen.initial_seed(), off0, MaskDraw.offset_step,
-                               state.base)
+    ops.sparta_torch_bernoulli(table, nblocks, float(selector.p), gen.initial_seed(), off0, MaskDraw.offset_step, out)
     gen.set_offset(off0 + MaskDraw.offset_step * state.ndrawn)
+    return bits
 
 
 class ShuffledSequentialIndexSelector(IndexSelector):
@@ -273,9 +290,11 @@ class SparseCommunicator(CommunicationModule):
         a = s.arena
         if self._mask is None:
             self._mask = torch.zeros(a.n, dtype=torch.uint8, device=a.device)
+            self._bits = torch.zeros(ops.sparta_mask_words(a.n), dtype=torch.int64, device=a.device)
         skip = {i for i, p in enumerate(a.params) if not p.requires_grad or p.grad is None}
-        draw_masks(self.index_selector, a.params, a.layout.views(self._mask), skip, self.iteration, self._draw)
-        return self._mask
+        packed = draw_masks(self.index_selector, a.params, a.layout.views(self._mask), skip, self.iteration,
+                            self._draw, bits=self._bits)
+        return self._mask if packed is None else packed
 
     def _mask_cap(self):
         """Selected-count bound for Bernoulli masks (no host sync per step);

@@ -146,12 +146,15 @@ GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, h
  * workgroup}, workgroups of 256 lanes, each lane one 4-element group,
  * nblocks in total) uses generator offset offset0 + i * offset_step; element
  * 4t + j of the tensor is selected iff the j-th uniform of Philox4x32-10
- * (key seed, counter {offset/4, t}) is <= p.  mask[offset + e] <- 0/1.
- * The caller advances the torch generator by ntens * offset_step.
+ * (key seed, counter {offset/4, t}) is <= p.  GA_MASK_BYTES: mask[offset + e]
+ * <- 0/1; GA_MASK_BITS (arena offsets multiples of 64): the tensor's bits of
+ * the packed words (ga_sparta_pack_mask layout; words of tensors not drawn
+ * are left as they are).  The caller advances the torch generator by
+ * ntens * offset_step.
  */
 GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
-                                     uint64_t seed, uint64_t offset0, uint64_t offset_step, uint8_t* mask,
-                                     hipStream_t stream);
+                                     uint64_t seed, uint64_t offset0, uint64_t offset_step, void* mask,
+                                     int mask_format, hipStream_t stream);
 
 /*
  * Select the SPARTA index set over an arena of n elements and gather the

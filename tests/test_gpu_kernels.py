@@ -893,6 +893,7 @@ def test_sparta_inplace_bernoulli_is_the_reference_draw(mode):
     p)).bool() bits (sparta.py:80-85) and leaves the generator where the
     reference leaves it, step after step, on GPT-2-like shapes with a
     grad-less tensor skipped."""
+    from gym_amd import ops
     from gym_amd.arena import ArenaLayout
     from gym_amd.strategy.sparta import MaskDraw, RandomIndexSelector, draw_masks
     shapes = [(50304, 768), (1024, 768), (768,), (2304, 768), (2304,), (3072, 768), (66, 128), (3, 5, 7), (1,)]
@@ -911,8 +912,17 @@ def test_sparta_inplace_bernoulli_is_the_reference_draw(mode):
         after_ref = torch.cuda.get_rng_state()
         torch.cuda.set_rng_state(gen)
         mask.fill_(7)
-        draw_masks(sel, params, L.views(mask), skip, step, state)
+        bits = torch.full((ops.sparta_mask_words(L.n),), -1, dtype=torch.int64, device=DEV)
+        bits[-(-(L.offsets[-1] + L.numels[-1]) // 64):] = 0  # the arena's trailing words (zero from allocation)
+        packed = draw_masks(sel, params, L.views(mask), skip, step, state, bits=bits if step % 2 else None)
         assert torch.equal(torch.cuda.get_rng_state(), after_ref), step
+        if packed is not None:  # the fused draw wrote the packed words instead of the bytes
+            assert mode == "fused"
+            mask.copy_(torch.from_numpy(osparta.unpack_mask(packed.cpu().numpy(), L.n).astype(np.uint8)))
+            pad = np.ones(L.n, bool)
+            for o, nn in zip(L.offsets, L.numels):
+                pad[o:o + nn] = False
+            assert not mask.cpu().numpy()[pad].any()
         for i, v in enumerate(L.views(mask)):
             if i in skip:
                 assert int(v.sum()) == 0
@@ -943,3 +953,10 @@ def test_torch_gpu_bernoulli_oracle_and_kernel(numel, p):
     got = mask.cpu().numpy()
     assert np.array_equal(got[64:64 + numel] != 0, want) and set(np.unique(got[64:64 + numel])) <= {0, 1}
     assert (got[:64] == 9).all() and (got[64 + numel:] == 9).all()
+    # packed output: the tensor's words (tail bits past numel zero); neighbours untouched
+    words = ops.sparta_mask_words(64 + numel + 64)
+    bits = torch.full((words,), -1, dtype=torch.int64, device=DEV)
+    ops.sparta_torch_bernoulli(table, nb, p, seed, off, 12, bits)
+    gb = bits.cpu().numpy()
+    assert gb[0] == -1 and all(gb[w] == -1 for w in range(1 + -(-numel // 64), words))
+    assert np.array_equal(gb[1:1 + -(-numel // 64)], osparta.pack_mask(want))
