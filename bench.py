@@ -342,8 +342,8 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
 
     def step():
         if mask_source == "torch":
-            packed = draw_masks(sel, mviews, mviews, set(), it[0], draw, bits=mbits)
-            eng(reps, mask=mask if packed is None else packed, mask_cap=eng.cap)
+            packed = draw_masks(sel, mviews, mviews, set(), it[0], draw, bits=mbits, coll=coll)
+            eng(reps, mask=mask if packed is None else packed, mask_cap=eng.cap, mask_shared=packed is not None)
         else:
             eng(reps, seed=42, iteration=it[0])
         it[0] += 1
@@ -379,8 +379,8 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     if mask_source == "torch":
         out["mask"] = ("the reference's per-tensor torch.bernoulli draws, bit-identical, as one "
                        "ga_sparta_torch_bernoulli launch writing the packed mask, in the step" +
-                       ("" if coll.world == 1 else f"; rank 0's broadcast: "
-                        f"{ops.sparta_mask_words(layout.n) * 8} B instead of the reference's {layout.n} B"))
+                       ("" if coll.world == 1 else "; every rank draws rank 0's masks from its broadcast generator "
+                        f"state: 16 B on the wire instead of the reference's {layout.n} B of masks"))
     if queued is not None:
         out["kernel_ms"] = round(queued, 4)
         out["kernel_alg_GBps"] = round(alg / (queued * 1e-3) / 1e9, 1)

@@ -667,7 +667,13 @@ __global__ __launch_bounds__(kSpBlock) void sparta_pack_mask_kernel(const uint8_
 template <bool BITS>
 __global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const int64_t* __restrict__ tab, int ntens,
                                                                          float p, uint2 key, uint64_t off0,
-                                                                         uint64_t step, void* __restrict__ mask) {
+                                                                         uint64_t step, const uint64_t* seedoff,
+                                                                         void* __restrict__ mask) {
+    if (seedoff) {  // the generator state as rank 0 broadcast it (device memory)
+        const uint64_t sd = seedoff[0];
+        key = make_uint2((uint32_t)sd, (uint32_t)(sd >> 32));
+        off0 = seedoff[1];
+    }
     const int b = (int)blockIdx.x;
     int lo = 0, hi = ntens - 1;
     while (lo < hi) {  // last row whose first workgroup <= b
@@ -858,8 +864,9 @@ extern "C" GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64
 }
 
 extern "C" GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
-                                                uint64_t seed, uint64_t offset0, uint64_t offset_step, void* mask,
-                                                int mask_format, hipStream_t stream) {
+                                                uint64_t seed, uint64_t offset0, uint64_t offset_step,
+                                                const uint64_t* seedoff, void* mask, int mask_format,
+                                                hipStream_t stream) {
     clear_error();
     GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS,
                "ga_sparta_torch_bernoulli: bad mask_format %d", mask_format);
@@ -870,7 +877,7 @@ extern "C" GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t nt
     GA_REQUIRE(table && mask && ((uintptr_t)mask % 8) == 0, "ga_sparta_torch_bernoulli: null table/mask or mask alignment");
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kSpBlock), 0, stream, table, (int)ntens, p,
-                           make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)), offset0, offset_step, mask);
+                           make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)), offset0, offset_step, seedoff, mask);
     };
     if (mask_format == GA_MASK_BITS) go(sparta_torch_bernoulli_kernel<true>);
     else go(sparta_torch_bernoulli_kernel<false>);

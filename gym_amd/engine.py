@@ -274,7 +274,7 @@ class Sparta:
             if int(self._flag_host[1]) != 0:
                 raise RuntimeError(f"SPARTA: {int(self._flag_host[0])} elements selected > capacity {self.cap}")
 
-    def __call__(self, reps, seed=0, iteration=0, mask=None, skip=None, mask_cap=None):
+    def __call__(self, reps, seed=0, iteration=0, mask=None, skip=None, mask_cap=None, mask_shared=False):
         """mask: this process's uint8/bool mask arena (the reference selector's
         draws), or its packed int64 words, or None for the Philox stream.  With an exchange, rank 0's mask
         wins (sparta.py:32-37): it is packed to one bit per element and
@@ -282,13 +282,16 @@ class Sparta:
         mask_cap: a bound on the selected count that holds on every rank (e.g.
         sparta_capacity for Bernoulli masks): no host sync for the exact count,
         overflow flagged on the device as in Philox mode.  None: the exact
-        count is read back (any selector)."""
+        count is read back (any selector).
+        mask_shared: the mask is already rank 0's on every rank (the fused
+        reference draw from rank 0's broadcast generator state): no mask
+        broadcast."""
         n = self.n
         cnt = None
         if mask is not None and mask.dtype == torch.int64:  # already packed (the fused reference draw)
             if mask_cap is None:
                 raise ValueError("Sparta: a packed mask needs mask_cap")
-            if self.coll.exchange:
+            if self.coll.exchange and not mask_shared:
                 self.coll.broadcast_(mask[:ops.sparta_mask_words(n)], 0)
         elif mask is not None and self.coll.exchange:
             words = ops.sparta_mask_words(n)

@@ -148,19 +148,24 @@ def sparta_bernoulli_table(offsets, numels, device):
     return t, b
 
 
-def sparta_torch_bernoulli(table, nblocks, p, seed, offset0, offset_step, mask):
+def sparta_torch_bernoulli(table, nblocks, p, seed, offset0, offset_step, mask, seedoff=None):
     """Element e of drawn tensor i <- torch.bernoulli(torch.full(shape_i, p))
     element e as ATen's HIP kernel draws it with generator (seed, offset0 + i *
     offset_step); every drawn tensor in one launch.  mask: the uint8 arena
-    (byte at arena offset + e) or int64 packed words (bit arena offset + e)."""
-    _gpu(table, mask)
+    (byte at arena offset + e) or int64 packed words (bit arena offset + e).
+    seedoff: optional int64 [2] device tensor {seed, offset0} read by the
+    kernel instead of the two arguments (rank 0's generator state, broadcast)."""
+    _gpu(table, mask, seedoff)
+    if seedoff is not None and (seedoff.dtype != torch.int64 or seedoff.numel() < 2):
+        raise ValueError("sparta_torch_bernoulli: seedoff must be an int64 [2] tensor")
     if mask.dtype not in (torch.uint8, torch.int64) or not mask.is_contiguous():
         raise ValueError("sparta_torch_bernoulli: mask must be a contiguous uint8 arena or int64 packed words")
     fmt = _lib.GA_MASK_BITS if mask.dtype == torch.int64 else _lib.GA_MASK_BYTES
     if table.dtype != torch.int64 or table.dim() != 2 or table.shape[1] != 3 or not table.is_contiguous():
         raise ValueError("sparta_torch_bernoulli: table must be a contiguous int64 [T, 3] tensor")
     check(lib().ga_sparta_torch_bernoulli(_p(table), int(table.shape[0]), int(nblocks), float(p),
-                                          int(seed) & (2**64 - 1), int(offset0), int(offset_step), _p(mask), fmt,
+                                          int(seed) & (2**64 - 1), int(offset0), int(offset_step), _p(seedoff),
+                                          _p(mask), fmt,
                                           _stream()), "ga_sparta_torch_bernoulli")
 
 

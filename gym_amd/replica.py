@@ -174,8 +174,9 @@ class ReplicaRunner:
                 self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
             else:
                 sel = s.index_selector
-                self.sparta(P, mask=self._build_mask(),
-                            mask_cap=self.sparta.cap if type(sel) is RandomIndexSelector else None)
+                m = self._build_mask()
+                self.sparta(P, mask=m, mask_cap=self.sparta.cap if type(sel) is RandomIndexSelector else None,
+                            mask_shared=self.mask_shared)
             self.iteration += 1
         elif isinstance(s, FedAvgStrategy):
             self._inner()
@@ -210,7 +211,8 @@ class ReplicaRunner:
         process's and broadcasts it to the others."""
         a0 = self.ra.arenas[0]
         packed = draw_masks(self.s.index_selector, a0.params, self.ra.layout.views(self.mask), set(self._grad_less()),
-                            self.iteration, self.draw, bits=self.bits)
+                            self.iteration, self.draw, bits=self.bits, coll=self.coll)
+        self.mask_shared = packed is not None
         return self.mask if packed is None else packed
 
     def _inner(self):

@@ -80,12 +80,17 @@ class MaskDraw:
         self.table = None
 
 
-def draw_masks(selector, params, views, skip, iteration, state, bits=None):
+def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=None):
     """Every tensor's selector mask into its view of a uint8 mask arena, in
     parameter order (sparta.py:28-33); tensors in `skip` stay 0.  Returns the
     mask to select with: `bits` (int64 packed words of the same arena,
     ga_sparta_pack_mask layout) when the fused GPU draw wrote them there
     instead of the bytes, else None (the uint8 arena holds the masks).
+    coll (a Collective with an exchange): the fused draw uses rank 0's
+    generator state, broadcast (16 bytes), so the returned packed mask is
+    already rank 0's on every rank (the reference broadcasts the masks,
+    sparta.py:32-37); every rank's own generator still advances as its own
+    draws would advance it.
 
     RandomIndexSelector on a GPU: one ga_sparta_torch_bernoulli launch draws
     every tensor's mask exactly as the per-tensor torch.bernoulli calls would
@@ -123,7 +128,7 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None):
 
     on_gpu = bool(params) and params[0].device.type == "cuda"
     if on_gpu and MaskDraw.fused:
-        out = _draw_fused(selector, params, views, skip, state, bits)
+        out = _draw_fused(selector, params, views, skip, state, bits, coll)
         state.calls += 1
         return out
     for i, p in enumerate(params):
@@ -141,7 +146,12 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None):
     state.calls += 1
 
 
-def _draw_fused(selector, params, views, skip, state, bits=None):
+def _i64(v):
+    v = int(v) & (2**64 - 1)
+    return v - 2**64 if v >= 2**63 else v
+
+
+def _draw_fused(selector, params, views, skip, state, bits=None, coll=None):
     """Every drawn tensor's torch.bernoulli(torch.full(shape, p)) in ONE launch
     (ga_sparta_torch_bernoulli: ATen's HIP kernel for it restated, bit for
     bit), with the default generator of the device read and advanced exactly
@@ -174,7 +184,16 @@ def _draw_fused(selector, params, views, skip, state, bits=None):
     dev = state.base.device
     gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
     off0 = gen.get_offset()
-    ops.sparta_torch_bernoulli(table, nblocks, float(selector.p), gen.initial_seed(), off0, MaskDraw.offset_step, out)
+    seedoff = None
+    if coll is not None and coll.exchange:  # rank 0's generator state, 16 bytes on the wire
+        if getattr(state, "seedoff", None) is None:
+            state.seedoff = torch.zeros(2, dtype=torch.int64, device=dev)
+        state.seedoff[0].fill_(_i64(gen.initial_seed()))
+        state.seedoff[1].fill_(_i64(off0))
+        coll.broadcast_(state.seedoff, 0)
+        seedoff = state.seedoff
+    ops.sparta_torch_bernoulli(table, nblocks, float(selector.p), gen.initial_seed(), off0, MaskDraw.offset_step, out,
+                               seedoff=seedoff)
     gen.set_offset(off0 + MaskDraw.offset_step * state.ndrawn)
     return bits
 
@@ -293,7 +312,8 @@ class SparseCommunicator(CommunicationModule):
             self._bits = torch.zeros(ops.sparta_mask_words(a.n), dtype=torch.int64, device=a.device)
         skip = {i for i, p in enumerate(a.params) if not p.requires_grad or p.grad is None}
         packed = draw_masks(self.index_selector, a.params, a.layout.views(self._mask), skip, self.iteration,
-                            self._draw, bits=self._bits)
+                            self._draw, bits=self._bits, coll=s.coll)
+        self._shared = packed is not None
         return self._mask if packed is None else packed
 
     def _mask_cap(self):
@@ -319,7 +339,8 @@ class SparseCommunicator(CommunicationModule):
                 if self._philox_mode():
                     self._engine(reps, seed=self._shared_seed(), iteration=self.iteration, skip=self._skip_table())
                 else:
-                    self._engine(reps, mask=self._build_mask(model), mask_cap=self._mask_cap())
+                    m = self._build_mask(model)
+                    self._engine(reps, mask=m, mask_cap=self._mask_cap(), mask_shared=self._shared)
         self.iteration += 1
 
 

@@ -149,12 +149,16 @@ GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, h
  * (key seed, counter {offset/4, t}) is <= p.  GA_MASK_BYTES: mask[offset + e]
  * <- 0/1; GA_MASK_BITS (arena offsets multiples of 64): the tensor's bits of
  * the packed words (ga_sparta_pack_mask layout; words of tensors not drawn
- * are left as they are).  The caller advances the torch generator by
- * ntens * offset_step.
+ * are left as they are).  If seedoff != null (device memory, {seed,
+ * offset0}) those replace the seed/offset0 arguments: the generator state rank
+ * 0 broadcast (16 bytes), so every rank draws rank 0's masks (the reference
+ * broadcasts the masks themselves, sparta.py:32-37).  The caller advances its
+ * torch generator by ntens * offset_step.
  */
 GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
-                                     uint64_t seed, uint64_t offset0, uint64_t offset_step, void* mask,
-                                     int mask_format, hipStream_t stream);
+                                     uint64_t seed, uint64_t offset0, uint64_t offset_step,
+                                     const uint64_t* seedoff, void* mask, int mask_format,
+                                     hipStream_t stream);
 
 /*
  * Select the SPARTA index set over an arena of n elements and gather the

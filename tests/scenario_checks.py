@@ -88,9 +88,14 @@ def _torch_masks(kind, device, steps):
     return masks
 
 
-def check_sparta_sel(res, world, golden_dir, kind="random", device="cpu"):
+def check_sparta_sel(res, world, golden_dir, kind="random", device="cpu", rank_seeds=False):
     import strategy_scenarios as S
     nt = len(S.SEL_SHAPES)
+    if kind == "random" and "gen_0" in res[0]:  # every rank's generator advanced by its own draws
+        draws = S.SEL_STEPS * (nt - 1)
+        for r in range(world):
+            seed, off = (int(v) for v in res[r]["gen_0"])
+            assert seed == 42 + (r if rank_seeds else 0) and off == 12 * draws, (r, seed, off)
     if kind == "philox":
         seed = int(res[0]["seed_0"])
         offs = res[0]["offsets_0"]

@@ -160,13 +160,16 @@ def make_selector(kind):
     return RandomIndexSelector(p, mask_source="philox" if kind == "philox" else "torch")
 
 
-def sc_sparta_sel(rank, world, dev, golden_dir, kind="random"):
+def sc_sparta_sel(rank, world, dev, golden_dir, kind="random", rank_seeds=False):
     """SparseCommunicator with each index selector, driven the way a reference
     user builds it (CommunicateOptimizeStrategy([SparseCommunicator(sel)])),
-    plus a frozen tensor that must be left alone."""
+    plus a frozen tensor that must be left alone.  rank_seeds: every rank
+    seeds its generator differently -- rank 0's masks must still win
+    (sparta.py:32-37) and every rank's generator must advance by its own
+    draws."""
     from gym_amd.strategy import CommunicateOptimizeStrategy, OptimSpec
     from gym_amd.strategy.sparta import SparseCommunicator
-    torch.manual_seed(42)  # TrainNode seeds every rank (train_node.py:50-53)
+    torch.manual_seed(42 + (rank if rank_seeds else 0))  # TrainNode seeds every rank (train_node.py:50-53)
     model = ShapeModel(SEL_SHAPES, seed=300 + rank).to(dev)
     model.ps[SEL_FROZEN].requires_grad_(False)
     comm = SparseCommunicator(make_selector(kind))
@@ -182,6 +185,9 @@ def sc_sparta_sel(rank, world, dev, golden_dir, kind="random"):
     if kind == "philox":
         out["seed"] = [np.array(comm._seed, dtype=np.int64)]
         out["offsets"] = [np.array(s.arena.layout.offsets, dtype=np.int64)]
+    if torch.device(dev).type == "cuda":
+        gen = torch.cuda.default_generators[torch.device(dev).index or 0]
+        out["gen"] = [np.array([gen.initial_seed(), gen.get_offset()], dtype=np.uint64)]
     return {f"{k}_{i}": v for k, lst in out.items() for i, v in enumerate(lst)}
 
 

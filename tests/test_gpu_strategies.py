@@ -20,6 +20,7 @@ CASES = [
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": True}),
     ("sparta_philox", 2, {}),
     ("sparta_sel", 2, {"kind": "random"}), ("sparta_sel", 3, {"kind": "random"}),
+    ("sparta_sel", 3, {"kind": "random", "rank_seeds": True}),
     ("sparta_sel", 2, {"kind": "shuffled"}), ("sparta_sel", 2, {"kind": "partitioned"}),
     ("sparta_sel", 3, {"kind": "philox"}),
     ("eval_avg", 2, {}), ("eval_avg", 3, {}),
@@ -34,7 +35,7 @@ def test_strategy_on_gpu(tmp_path, name, world, kw):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = S.run(name, world, "cuda:0", False, str(tmp_path), GOLDEN, **kw)
-    check_kw = {k: kw[k] for k in ("island_size", "kind") if k in kw}
+    check_kw = {k: kw[k] for k in ("island_size", "kind", "rank_seeds") if k in kw}
     if name == "sparta_sel":
         check_kw["device"] = "cuda:0"
     CHECKS[name](res, world, GOLDEN, **check_kw)

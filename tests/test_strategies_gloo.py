@@ -17,6 +17,7 @@ CASES = [
     ("sparta", 2, {"replay": True}), ("sparta", 3, {"replay": False}),
     ("sparta_philox", 2, {}),
     ("sparta_sel", 2, {"kind": "random"}), ("sparta_sel", 3, {"kind": "random"}),
+    ("sparta_sel", 3, {"kind": "random", "rank_seeds": True}),
     ("sparta_sel", 2, {"kind": "shuffled"}), ("sparta_sel", 2, {"kind": "partitioned"}),
     ("sparta_sel", 3, {"kind": "philox"}),
     ("eval_avg", 2, {}), ("eval_avg", 3, {}),
@@ -30,7 +31,7 @@ CASES = [
 @pytest.mark.parametrize("name,world,kw", CASES, ids=[f"{c[0]}-w{c[1]}-{c[2]}" for c in CASES])
 def test_strategy_orchestration_gloo(tmp_path, name, world, kw):
     res = S.run(name, world, "cpu", True, str(tmp_path), GOLDEN, **kw)
-    check_kw = {k: kw[k] for k in ("island_size", "kind") if k in kw}
+    check_kw = {k: kw[k] for k in ("island_size", "kind", "rank_seeds") if k in kw}
     if name == "sparta_sel":
         check_kw["device"] = "cpu"
     CHECKS[name](res, world, GOLDEN, **check_kw)
