@@ -55,6 +55,7 @@ SIGNATURES = {
     "ga_sparta_workspace_bytes": (c_i64, [c_i64]),
     "ga_sparta_gap_table": (None, [c_f64, c_p]),
     "ga_sparta_pack_mask": (c_i32, [c_p, c_i64, c_p, c_p]),
+    "ga_sparta_torch_bernoulli_span": (c_i64, []),
     "ga_sparta_torch_bernoulli": (c_i32, [c_p, c_i32, c_i64, c_f32, c_u64, c_u64, c_u64, c_p, c_p, c_i32, c_p]),
     "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_i32, c_u64, c_u64, c_f64, c_p, c_i64,
                                  c_i64, c_p, c_p, c_p, c_p, c_p]),

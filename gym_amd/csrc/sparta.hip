@@ -43,7 +43,9 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
     for (int r = 0; r < 10; ++r) {
         const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
         const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
-        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        // 3-input XORs as one gfx950 v_bitop3_b32 each (LUT 0x96 = a ^ b ^ c)
+        c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k.x, 0x96), lo1,
+                       __builtin_amdgcn_bitop3_b32(hi0, c.w, k.y, 0x96), lo0);
         k.x += W0;
         k.y += W1;
     }
@@ -664,6 +666,12 @@ __global__ __launch_bounds__(kSpBlock) void sparta_pack_mask_kernel(const uint8_
 // generator offset torch hands out per bernoulli_ call.  One lane per
 // 4-element group; a workgroup stays inside one tensor (table rows: arena
 // offset, numel, first workgroup), so the lookup is a uniform binary search.
+#ifndef GA_TB_CALLS
+#define GA_TB_CALLS 4
+#endif
+constexpr int kTbCalls = GA_TB_CALLS;                 // Philox calls (4-element groups) per lane
+constexpr int64_t kTbSpan = 4 * kSpBlock * kTbCalls;  // elements per workgroup
+
 template <bool BITS>
 __global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const int64_t* __restrict__ tab, int ntens,
                                                                          float p, uint2 key, uint64_t off0,
@@ -682,37 +690,41 @@ __global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const 
         else hi = mid - 1;
     }
     const int64_t base = tab[3 * lo], numel = tab[3 * lo + 1];
-    const uint64_t t = (uint64_t)(b - tab[3 * lo + 2]) * kSpBlock + threadIdx.x;
-    const int64_t e0 = (int64_t)t * 4;
-    uint32_t v[4] = {0u, 0u, 0u, 0u};
-    if (e0 < numel) {
-        const uint64_t ctr = (off0 + (uint64_t)lo * step) >> 2;
-        const uint4 w = philox4x32_10(
-            make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)), key);
-        const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
-        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    const uint64_t t0 = (uint64_t)(b - tab[3 * lo + 2]) * kSpBlock * kTbCalls + threadIdx.x;
+    const uint64_t ctr = (off0 + (uint64_t)lo * step) >> 2;
+    const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
+    uint4 w[kTbCalls];
+#pragma unroll
+    for (int c = 0; c < kTbCalls; ++c) {  // independent chains: the calls interleave
+        const uint64_t t = t0 + (uint64_t)c * kSpBlock;
+        w[c] = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)), key);
+    }
+#pragma unroll
+    for (int c = 0; c < kTbCalls; ++c) {
+        const int64_t e0 = (int64_t)(t0 + (uint64_t)c * kSpBlock) * 4;
+        const uint32_t ws[4] = {w[c].x, w[c].y, w[c].z, w[c].w};
+        uint32_t v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = (e0 + j < numel && (inv + (float)ws[j] * inv) <= p) ? 1u : 0u;
-    }
-    if constexpr (BITS) {
-        // 16 consecutive lanes = one 64-element word (t % 16 == 0 at lane 16q; base % 64 == 0)
-        const int sh = 4 * (int)(threadIdx.x & 15);
-        const uint32_t nib = v[0] | (v[1] << 1) | (v[2] << 2) | (v[3] << 3);
-        uint32_t lo32 = sh < 32 ? nib << sh : 0u, hi32 = sh >= 32 ? nib << (sh - 32) : 0u;
+        if constexpr (BITS) {
+            // 16 consecutive lanes = one 64-element word (t % 16 == 0 at lane 16q; base % 64 == 0)
+            const int sh = 4 * (int)(threadIdx.x & 15);
+            const uint32_t nib = v[0] | (v[1] << 1) | (v[2] << 2) | (v[3] << 3);
+            uint32_t lo32 = sh < 32 ? nib << sh : 0u, hi32 = sh >= 32 ? nib << (sh - 32) : 0u;
 #pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            lo32 |= (uint32_t)__shfl_xor((int)lo32, d, 64);
-            hi32 |= (uint32_t)__shfl_xor((int)hi32, d, 64);
-        }
-        if ((threadIdx.x & 15) == 0 && e0 < numel)
-            reinterpret_cast<uint64_t*>(mask)[(base + e0) >> 6] = ((uint64_t)hi32 << 32) | lo32;
-    } else {
-        if (e0 >= numel) return;
-        uint8_t* m = reinterpret_cast<uint8_t*>(mask) + base + e0;
-        if (e0 + 4 <= numel) {
-            *reinterpret_cast<uchar4*>(m) = make_uchar4(v[0], v[1], v[2], v[3]);
-        } else {
-            for (int j = 0; e0 + j < numel; ++j) m[j] = (uint8_t)v[j];
+            for (int d = 1; d < 16; d <<= 1) {
+                lo32 |= (uint32_t)__shfl_xor((int)lo32, d, 64);
+                hi32 |= (uint32_t)__shfl_xor((int)hi32, d, 64);
+            }
+            if ((threadIdx.x & 15) == 0 && e0 < numel)
+                reinterpret_cast<uint64_t*>(mask)[(base + e0) >> 6] = ((uint64_t)hi32 << 32) | lo32;
+        } else if (e0 < numel) {
+            uint8_t* m = reinterpret_cast<uint8_t*>(mask) + base + e0;
+            if (e0 + 4 <= numel) {
+                *reinterpret_cast<uchar4*>(m) = make_uchar4(v[0], v[1], v[2], v[3]);
+            } else {
+                for (int j = 0; e0 + j < numel; ++j) m[j] = (uint8_t)v[j];
+            }
         }
     }
 }
@@ -862,6 +874,8 @@ extern "C" GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64
                        stream, mask, n, bits);
     return check_launch("ga_sparta_pack_mask");
 }
+
+extern "C" GA_API int64_t ga_sparta_torch_bernoulli_span(void) { return kTbSpan; }
 
 extern "C" GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
                                                 uint64_t seed, uint64_t offset0, uint64_t offset_step,

@@ -130,15 +130,12 @@ def sparta_pack_mask(mask, n, bits):
     check(lib().ga_sparta_pack_mask(_p(mask), int(n), _p(bits), _stream()), "ga_sparta_pack_mask")
 
 
-TORCH_BERNOULLI_BLOCK = 256  # lanes per workgroup of ga_sparta_torch_bernoulli (4 elements per lane)
-
-
 def sparta_bernoulli_table(offsets, numels, device):
     """(int64 [T, 3] device table, workgroups) for ga_sparta_torch_bernoulli:
     per drawn tensor its arena offset (a multiple of 64: the packed form's
     words never straddle tensors), numel and first workgroup."""
     rows, b = [], 0
-    per = 4 * TORCH_BERNOULLI_BLOCK
+    per = int(lib().ga_sparta_torch_bernoulli_span())
     for o, n in zip(offsets, numels):
         if o % 64:
             raise ValueError("sparta_bernoulli_table: arena offsets must be multiples of 64")

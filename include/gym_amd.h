@@ -142,9 +142,9 @@ GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, h
  * The reference's per-tensor mask draw, RandomIndexSelector.get_indices =
  * torch.bernoulli(torch.full(shape, p, device=cuda)) (sparta.py:80-85), for
  * every drawn tensor in one launch, bit-identical to ATen's HIP kernel for it:
- * tensor i (table row i = {arena offset (a multiple of 4), numel, first
- * workgroup}, workgroups of 256 lanes, each lane one 4-element group,
- * nblocks in total) uses generator offset offset0 + i * offset_step; element
+ * tensor i (table row i = {arena offset (a multiple of 64), numel, first
+ * workgroup}, each workgroup ga_sparta_torch_bernoulli_span() elements of one
+ * tensor, nblocks in total) uses generator offset offset0 + i * offset_step; element
  * 4t + j of the tensor is selected iff the j-th uniform of Philox4x32-10
  * (key seed, counter {offset/4, t}) is <= p.  GA_MASK_BYTES: mask[offset + e]
  * <- 0/1; GA_MASK_BITS (arena offsets multiples of 64): the tensor's bits of
@@ -155,6 +155,9 @@ GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, h
  * broadcasts the masks themselves, sparta.py:32-37).  The caller advances its
  * torch generator by ntens * offset_step.
  */
+/* Elements per workgroup of ga_sparta_torch_bernoulli (the table's first-workgroup unit). */
+GA_API int64_t ga_sparta_torch_bernoulli_span(void);
+
 GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
                                      uint64_t seed, uint64_t offset0, uint64_t offset_step,
                                      const uint64_t* seedoff, void* mask, int mask_format,
