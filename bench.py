@@ -443,12 +443,19 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
     decn = tn.wrap(lambda: ops.demo_decode(plan, codec.payload[0:1], P, None, 1e-3))
     tn.on = True
     timed_loop(decn, args.steps, args.warmup, coll)
+    pipe_ms = None
+    if coll.exchange and coll.rccl:  # the exchange as the strategies run it: async all-gathers of tensor groups
+        from gym_amd.engine import DEMO_PIECES, PipelinedDeMoCodec
+        pipe = PipelinedDeMoCodec(coll, 1, layout, dev, pieces=DEMO_PIECES)
+        pipe_ms = timed_loop(lambda: pipe(P, G, D, 1e-3, 0.999, 0.0), args.steps, args.warmup, coll) * 1e3
+        del pipe
     n = numel(shapes)
     # algorithmic HBM bytes: encode reads delta, g and writes delta (wd = 0) + the
     # payload; decode reads p, writes p and grad + S payloads (8 B per entry)
     enc_bytes = 12 * n + 8 * plan.M
     dec_bytes = 12 * n + 8 * plan.M
     return {"ms_per_step": round(t * 1e3, 4), "model": model, "nodes": coll.world,
+            "ms_per_step_pipelined": round(pipe_ms, 4) if pipe_ms is not None else None,
             "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4), "decode_8src_ms": round(dec8_ms, 4),
             "decode_nograd_ms": round(tn.mean_ms(), 4),
             "encode_HBM_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .comm import Collective
+from .comm import DONE, Collective
 from .demo_codec import DemoPlan
 
 
@@ -367,3 +367,71 @@ class DeMoCodec:
         self.encode(P, G, D, lr, decay, weight_decay)
         self.exchange(all_gather)
         self.decode(P, G, lr)
+
+
+DEMO_PIECES = 4  # tensor groups of the pipelined DeMo exchange (RCCL, world > 1)
+
+
+def demo_codec(coll: Collective, K_local, layout, device, chunk=64, topk=32):
+    """The DeMo codec an exchange should use: pipelined over DEMO_PIECES tensor
+    groups when the all-gather is an async RCCL collective across processes,
+    else one encode -> all-gather -> decode."""
+    if coll.rccl and coll.exchange and DEMO_PIECES > 1 and len(layout.numels) > 1:
+        return PipelinedDeMoCodec(coll, K_local, layout, device, chunk=chunk, topk=topk, pieces=DEMO_PIECES)
+    return DeMoCodec(coll, K_local, layout, device, chunk=chunk, topk=topk)
+
+
+def split_tensors(numels, pieces):
+    """Contiguous groups of tensor indices with about equal element counts
+    (at most `pieces` groups, none empty)."""
+    total = sum(numels)
+    groups, cur, acc = [], [], 0
+    for i, n in enumerate(numels):
+        cur.append(i)
+        acc += n
+        if len(groups) < pieces - 1 and acc * pieces >= total * (len(groups) + 1):
+            groups.append(cur)
+            cur = []
+    if cur:
+        groups.append(cur)
+    return groups
+
+
+class PipelinedDeMoCodec:
+    """DeMoCodec over P groups of whole tensors, software-pipelined across the
+    exchange: piece p's all-gather (RCCL, async) runs while piece p+1 is
+    encoded and piece p-1 decoded, so at G GPUs the ~(G-1)/G of the payload
+    crossing xGMI hides behind the codec kernels.  Each piece is a codec of its
+    own over a subset of the tensors (same arena offsets, its own payload
+    [idx m_p | val m_p]); per chunk the arithmetic, the entries and the source
+    order are the ones of the unpipelined codec, so results are identical.
+    Same call signature as DeMoCodec.__call__ (no custom all_gather)."""
+
+    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32, pieces=4):
+        self.coll = coll
+        groups = split_tensors(layout.numels, max(1, int(pieces)))
+        self.codecs = [DeMoCodec(coll, K_local, layout.subset(g), device, chunk=chunk, topk=topk) for g in groups]
+        # every piece runs the kernel family the whole plan would (the wave-per-chunk
+        # kernels only if every chunk of the model qualifies), so the results match
+        if not DemoPlan(layout, chunk=chunk, topk=topk).wave_encode:
+            for c in self.codecs:
+                c.plan.wave_encode = False
+        self.M = sum(c.plan.M for c in self.codecs)
+
+    def reference_bytes(self, val_itemsize=4):
+        return sum(c.plan.reference_bytes(val_itemsize) for c in self.codecs)
+
+    def __call__(self, P, G, D, lr, decay=0.999, weight_decay=0.0):
+        pending = []
+        for c in self.codecs:
+            c.encode(P, G, D, lr, decay, weight_decay)
+            w = (self.coll.all_gather_into(c.gathered.view(-1), c.payload.view(-1), async_op=True)
+                 if self.coll.exchange else DONE)
+            pending.append((c, w))
+            if len(pending) > 1:
+                cp, wp = pending.pop(0)
+                wp.wait()
+                cp.decode(P, G, lr)
+        for cp, wp in pending:
+            wp.wait()
+            cp.decode(P, G, lr)

@@ -28,7 +28,7 @@ from torch.utils.data import DataLoader
 from . import ops
 from .arena import ReplicaArena
 from .comm import Collective
-from .engine import DeMoCodec, DiLoCoOuter, MeanReduce, Sparta
+from .engine import DiLoCoOuter, MeanReduce, Sparta, demo_codec
 from .fused_optim import ArenaAdam, fusable
 from .strategy.demo import DeMoStrategy
 from .strategy.diloco import DiLoCoStrategy, fused_sgd_hparams
@@ -109,8 +109,8 @@ class ReplicaRunner:
             self.delta = torch.zeros_like(self.ra.flat_set)
             # the codec covers the trainable tensors only, as DeMo's param list (demo.py:99-117)
             live = [i for i, p in enumerate(self.ra.arenas[0].params) if p.requires_grad]
-            self.codec = DeMoCodec(self.coll, self.K, self.ra.layout.subset(live), dev,
-                                   chunk=kw["compression_chunk"], topk=kw["compression_topk"])
+            self.codec = demo_codec(self.coll, self.K, self.ra.layout.subset(live), dev,
+                                    chunk=kw["compression_chunk"], topk=kw["compression_topk"])
         else:
             spec = s.optim_spec if isinstance(s, SimpleReduceStrategy) else s.inner_optim_spec
             if fusable(spec.cls, spec.kwargs, self.ra):

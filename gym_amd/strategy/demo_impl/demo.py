@@ -27,7 +27,7 @@ import torch.distributed as dist
 from ...arena import ParamArena
 from ...comm import Collective
 from ...demo_codec import smaller_split as _get_smaller_split  # noqa: F401  (demo.py:489-498, same name)
-from ...engine import DeMoCodec
+from ...engine import DeMoCodec, PipelinedDeMoCodec, demo_codec
 
 _REQUIRE_GPU = True  # the CPU orchestration tests swap the kernels for oracle stand-ins
 
@@ -66,13 +66,18 @@ class DeMo(torch.optim.SGD):
         self.coll = Collective(process_group)
         self.arena = ParamArena(trainable, world=self.coll.world)
         self.delta_flat = torch.zeros_like(self.arena.flat)
-        self.codec = DeMoCodec(self.coll, 1, self.arena.layout, self.arena.device, chunk=compression_chunk,
-                               topk=compression_topk)
+        # pipelined over tensor groups when the all-gather is async RCCL (engine.demo_codec);
+        # a user-supplied custom_all_gather gets the one-exchange codec
+        self._codec_kw = dict(chunk=compression_chunk, topk=compression_topk)
+        self.codec = (demo_codec(self.coll, 1, self.arena.layout, self.arena.device, **self._codec_kw)
+                      if self._gather_fn() is None else
+                      DeMoCodec(self.coll, 1, self.arena.layout, self.arena.device, **self._codec_kw))
         self.demo_state = {}
         for p, d in zip(trainable, self.arena.layout.views(self.delta_flat)):
             self.demo_state[p] = {"step": 0, "delta": d}
         itemsize = torch.finfo(self.default_dtype).bits // 8
-        self._tx = self.codec.plan.reference_bytes(itemsize)
+        ref = self.codec.reference_bytes if isinstance(self.codec, PipelinedDeMoCodec) else self.codec.plan.reference_bytes
+        self._tx = ref(itemsize)
 
     def _gather_fn(self):
         from ..communicate import all_gather as ours
@@ -96,9 +101,12 @@ class DeMo(torch.optim.SGD):
         P = a.flat.view(1, -1)
         G = a.grad_flat.view(1, -1)
         D = self.delta_flat.view(1, -1)
-        self.codec.encode(P, G, D, lr, self.compression_decay, self.weight_decay)
-        self.codec.exchange(self._gather_fn())
-        self.codec.decode(P, G, lr)
+        if isinstance(self.codec, PipelinedDeMoCodec):
+            self.codec(P, G, D, lr, self.compression_decay, self.weight_decay)
+        else:
+            self.codec.encode(P, G, D, lr, self.compression_decay, self.weight_decay)
+            self.codec.exchange(self._gather_fn())
+            self.codec.decode(P, G, lr)
         self.data_transmit = self._tx
         self.data_receive = self._tx * self.coll.world
         return loss

@@ -217,6 +217,15 @@ def check_demo(res, world, golden_dir):
     tally.done()
 
 
+def check_demo_pipe(res, world, golden_dir, **_):
+    """The pipelined codec ends exactly where the one-exchange codec ends
+    (params, signs, residual deltas) on every rank, in more than one piece."""
+    for r in range(world):
+        assert int(res[r]["pipe_pieces"]) > 1
+        for what in ("p", "g", "d"):
+            assert np.array_equal(res[r][f"pipe_pipe_{what}"], res[r][f"pipe_plain_{what}"]), (r, what)
+
+
 def check_engine(res, world, golden_dir, K_local=3, **_):
     """Every node of every rank ends equal to the oracle over all K_total nodes
     (reordered fp32 sums: RCCL/gloo ring order, 1e-6 relative)."""
@@ -257,6 +266,7 @@ def check_engine(res, world, golden_dir, K_local=3, **_):
                 np.testing.assert_allclose(res[0]["demo_p"][k, off:off + m].reshape(shape)[ok], want_p[ok],
                                            rtol=0, atol=1e-7)
         tally.done()
+        check_demo_pipe(res, 1, golden_dir)
 
 
 def check_simple_adamw(res, world, golden_dir, steps=3):
@@ -283,4 +293,5 @@ def check_simple_adamw(res, world, golden_dir, steps=3):
 
 CHECKS = {"simple_adamw": check_simple_adamw, "engine": check_engine, "simple": check_simple, "diloco": check_diloco, "sparta": check_sparta,
           "sparta_philox": check_sparta_philox, "sparta_sel": check_sparta_sel,
-          "eval_avg": check_eval_avg, "mnist_diloco": check_mnist_diloco, "fedavg": check_fedavg, "demo": check_demo}
+          "eval_avg": check_eval_avg, "mnist_diloco": check_mnist_diloco, "fedavg": check_fedavg, "demo": check_demo,
+          "demo_pipe": check_demo_pipe}

@@ -373,13 +373,45 @@ def sc_engine(rank, world, dev, golden_dir, K_local=3, chunks=4, force=False):
         codec(P, G, D, 0.01)
         out["demo_p"] = _host(P)
         out["demo_sign"] = _host(G)
+        out.update(_demo_pipe_pair(coll, K_local, nodes, dev, pieces=2))
     return out
+
+
+def _demo_pipe_pair(coll, K_local, nodes, dev, pieces):
+    """The same DeMo step through DeMoCodec and PipelinedDeMoCodec (async
+    all-gathers of tensor groups overlapping the codec kernels)."""
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.engine import DeMoCodec, PipelinedDeMoCodec
+    L = ArenaLayout([(128, 128), (768,), (64, 192), (3, 64)])
+    G0 = torch.from_numpy(np.stack([engine_node(j, L.n, salt=6) for j in nodes])).to(dev)
+    D0 = torch.from_numpy(np.stack([engine_node(j, L.n, salt=7) for j in nodes]) * np.float32(0.01)).to(dev)
+    P0 = torch.from_numpy(np.stack([engine_node(0, L.n, salt=8)] * len(nodes))).to(dev)
+    for T in (G0, D0, P0):
+        for k in range(K_local):  # zero padding, as the arena keeps it
+            for o, m, o2 in zip(L.offsets, L.numels, L.offsets[1:] + [L.n]):
+                T[k, o + m:o2] = 0
+    out = {}
+    for tag, make in (("plain", lambda: DeMoCodec(coll, K_local, L, dev)),
+                      ("pipe", lambda: PipelinedDeMoCodec(coll, K_local, L, dev, pieces=pieces))):
+        P, G, D = P0.clone(), G0.clone(), D0.clone()
+        codec = make()
+        for _ in range(2):
+            codec(P, G, D, 0.01, 0.999, 0.1)
+        out.update({f"pipe_{tag}_p": _host(P), f"pipe_{tag}_g": _host(G), f"pipe_{tag}_d": _host(D)})
+    if tag == "pipe":
+        out["pipe_pieces"] = np.array(len(codec.codecs))
+    return out
+
+
+def sc_demo_pipe(rank, world, dev, golden_dir, pieces=3):
+    from gym_amd.comm import Collective
+    return _demo_pipe_pair(Collective(), 2, range(rank * 2, rank * 2 + 2), dev, pieces)
 
 
 SCENARIOS = {"simple_adamw": sc_simple_adamw, "engine": sc_engine, "simple": sc_simple, "diloco": sc_diloco, "sparta": sc_sparta, "sparta_philox": sc_sparta_philox,
              "sparta_sel": sc_sparta_sel, "eval_avg": sc_eval_avg,
              "mnist_diloco": sc_mnist_diloco,
-             "fedavg": sc_fedavg, "demo": sc_demo}
+             "fedavg": sc_fedavg, "demo": sc_demo, "demo_pipe": sc_demo_pipe}
 
 
 def _worker(rank, world, port, name, device, fake, out_dir, golden_dir, kwargs, backend="gloo"):

@@ -26,7 +26,7 @@ CASES = [
     ("eval_avg", 2, {}), ("eval_avg", 3, {}),
     ("mnist_diloco", 2, {}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}), ("fedavg", 4, {"island_size": 3}),
-    ("demo", 2, {}),
+    ("demo", 2, {}), ("demo_pipe", 2, {}), ("demo_pipe", 3, {"pieces": 2}),
 ]
 
 

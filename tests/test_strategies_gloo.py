@@ -24,7 +24,7 @@ CASES = [
     ("mnist_diloco", 2, {}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}), ("fedavg", 4, {"island_size": 2}),
     ("fedavg", 4, {"island_size": 3}),
-    ("demo", 2, {}),
+    ("demo", 2, {}), ("demo_pipe", 2, {}), ("demo_pipe", 3, {"pieces": 2}),
 ]
 
 
