@@ -69,6 +69,10 @@ def setup_dist(gpus):
             return Collective()
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if os.environ.get("GA_BENCH_FORCE_EXCHANGE") == "1":
+            # rehearsal of the multi-GPU code paths on one GPU: a world-1 RCCL group whose
+            # collectives are issued anyway (tests/test_gpu_rccl.py); not a measurement
+            return Collective(force_exchange=True)
     else:
         torch.cuda.set_device(0)
     return Collective()
@@ -636,6 +640,8 @@ def main():
     }
     if "xgmi" in head:
         line["xgmi"] = head["xgmi"]
+    if coll.exchange and coll.world == 1:
+        line["rehearsal"] = "world-1 RCCL group with forced exchange: the multi-GPU code paths, not a measurement"
     if extras:
         line["extras"] = extras
     print(json.dumps(line), flush=True)

@@ -369,7 +369,10 @@ class DeMoCodec:
         self.decode(P, G, lr)
 
 
-DEMO_PIECES = 4  # tensor groups of the pipelined DeMo exchange (RCCL, world > 1)
+import os as _os
+
+# tensor groups of the pipelined DeMo exchange (RCCL, world > 1); GA_DEMO_PIECES overrides
+DEMO_PIECES = int(_os.environ.get("GA_DEMO_PIECES", "2"))
 
 
 def demo_codec(coll: Collective, K_local, layout, device, chunk=64, topk=32):
