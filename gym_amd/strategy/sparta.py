@@ -127,14 +127,16 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
                 v.bernoulli_(state.pfull[i])
 
     on_gpu = bool(params) and params[0].device.type == "cuda"
-    if on_gpu and MaskDraw.fused:
+    # inside a user's graph capture the generator offsets are graph-relative: torch's own kernels then
+    if on_gpu and MaskDraw.fused and not torch.cuda.is_current_stream_capturing():
         out = _draw_fused(selector, params, views, skip, state, bits, coll)
         state.calls += 1
         return out
     for i, p in enumerate(params):
         if i not in skip and state.pfull[i] is None:
             state.pfull[i] = torch.full(p.shape, selector.p, device=p.device)
-    if on_gpu and MaskDraw.use_graphs and state.graph is None and state.calls >= 1:
+    if (on_gpu and MaskDraw.use_graphs and state.graph is None and state.calls >= 1
+            and not torch.cuda.is_current_stream_capturing()):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             body()
