@@ -346,7 +346,7 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
 
     def step():
         if mask_source == "torch":
-            packed = draw_masks(sel, mviews, mviews, set(), it[0], draw, bits=mbits, coll=coll)
+            packed = draw_masks(sel, mviews, mviews, set(), it[0], draw, bits=mbits, coll=coll, defer=True)
             eng(reps, mask=mask if packed is None else packed, mask_cap=eng.cap, mask_shared=packed is not None)
         else:
             eng(reps, seed=42, iteration=it[0])
@@ -381,8 +381,10 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
                    f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter",
            "mask_source": mask_source}
     if mask_source == "torch":
-        out["mask"] = ("the reference's per-tensor torch.bernoulli draws, bit-identical, as one "
-                       "ga_sparta_torch_bernoulli launch writing the packed mask, in the step" +
+        out["mask"] = ("the reference's per-tensor torch.bernoulli draws, bit-identical, " +
+                       ("drawn inside the average kernel (GA_MASK_TORCH), in the step" if coll.world == 1 and
+                        not coll.exchange else "as one ga_sparta_torch_bernoulli launch writing the packed mask, "
+                        "in the step") +
                        ("" if coll.world == 1 else "; every rank draws rank 0's masks from its broadcast generator "
                         f"state: 16 B on the wire instead of the reference's {layout.n} B of masks"))
     if queued is not None:

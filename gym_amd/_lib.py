@@ -20,10 +20,17 @@ GA_LAYOUT_ROWS = 0
 GA_LAYOUT_ELEM_MAJOR = 1
 GA_MASK_BYTES = 0
 GA_MASK_BITS = 1
+GA_MASK_TORCH = 2
 
 c_i32, c_i64, c_u32, c_u64, c_f32, c_f64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_float, ctypes.c_double)
 c_p = ctypes.c_void_p
+
+
+class TorchDraw(ctypes.Structure):
+    """Mirror of `ga_sparta_torch_draw` (include/gym_amd.h)."""
+    _fields_ = [("table", c_p), ("ntens", c_i32), ("p", c_f32), ("seed", c_u64), ("offset0", c_u64),
+                ("offset_step", c_u64), ("seedoff", c_p)]
 
 
 class DemoTensor(ctypes.Structure):
@@ -56,6 +63,7 @@ SIGNATURES = {
     "ga_sparta_gap_table": (None, [c_f64, c_p]),
     "ga_sparta_pack_mask": (c_i32, [c_p, c_i64, c_p, c_p]),
     "ga_sparta_torch_bernoulli_span": (c_i64, []),
+    "ga_sparta_torch_draw_bytes": (c_i32, []),
     "ga_sparta_torch_bernoulli": (c_i32, [c_p, c_i32, c_i64, c_f32, c_u64, c_u64, c_u64, c_p, c_p, c_i32, c_p]),
     "ga_sparta_select": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_i32, c_u64, c_u64, c_f64, c_p, c_i64,
                                  c_i64, c_p, c_p, c_p, c_p, c_p]),

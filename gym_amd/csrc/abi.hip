@@ -63,6 +63,6 @@ extern "C" GA_API int ga_stream_copy(const void* src, void* dst, int64_t nbytes,
     return ga::check_launch("ga_stream_copy");
 }
 
-extern "C" GA_API int ga_abi_version(void) { return 102; }
+extern "C" GA_API int ga_abi_version(void) { return 103; }
 
 extern "C" GA_API const char* ga_last_error(void) { return ga::g_err; }

@@ -55,6 +55,12 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 struct Pred {
     const uint8_t* mask;  // uint8 mask arena, or null
     const uint64_t* bits; // packed mask (bit j of word w = element 64 w + j), or null; both null -> Philox
+    const int64_t* ttab;  // GA_MASK_TORCH: the reference draw in-kernel (ga_sparta_torch_draw), or null
+    int32_t tn;
+    float tp;
+    uint64_t toff0, tstep;
+    const uint64_t* tseedoff;
+    uint2 tkey;
     uint2 key;
     uint32_t it_lo, it_hi;
     const int64_t* skip;  // Philox: sorted disjoint [lo, hi) element ranges never selected
@@ -92,10 +98,60 @@ __device__ __forceinline__ int gap_of(const uint64_t* tab, uint32_t u) {
     return t;
 }
 
+// GA_MASK_TORCH: the 64 elements at e0 as ga_sparta_torch_bernoulli draws them
+// (tensor offsets are multiples of 64, so the group lies in one tensor or in
+// padding / a tensor not drawn): 16 Philox calls, four chains at a time
+__device__ __forceinline__ uint64_t torch_bits64(const Pred& P, int64_t e0) {
+    int lo = 0, hi = P.tn - 1;
+    while (lo < hi) {  // last drawn tensor starting at or before e0
+        const int mid = (lo + hi + 1) >> 1;
+        if (P.ttab[3 * mid] <= e0) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t base = P.ttab[3 * lo], numel = P.ttab[3 * lo + 1];
+    if (e0 < base || e0 >= base + numel) return 0ull;
+    uint2 key = P.tkey;
+    uint64_t off0 = P.toff0;
+    if (P.tseedoff) {
+        const uint64_t sd = P.tseedoff[0];
+        key = make_uint2((uint32_t)sd, (uint32_t)(sd >> 32));
+        off0 = P.tseedoff[1];
+    }
+    const uint64_t ctr = (off0 + (uint64_t)lo * P.tstep) >> 2;
+    const int64_t rel = e0 - base;
+    const uint64_t t0 = (uint64_t)rel >> 2;
+    const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
+    uint64_t bits = 0;
+#pragma unroll
+    for (int c0 = 0; c0 < 16; c0 += 4) {
+        uint4 w[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint64_t t = t0 + c0 + c;
+            w[c] = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
+                                 key);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t ws[4] = {w[c].x, w[c].y, w[c].z, w[c].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int e = 4 * (c0 + c) + j;
+                if (rel + e < numel && (inv + (float)ws[j] * inv) <= P.tp) bits |= 1ull << e;
+            }
+        }
+    }
+    return bits;
+}
+
 // Selection bits of the 64 elements starting at element `e0` (e0 % 64 == 0);
 // tab: the gap table in LDS.
 __device__ __forceinline__ uint64_t pred_bits64(const Pred& P, const uint64_t* tab, int64_t e0, int64_t n) {
     uint64_t bits = 0;
+    if (P.ttab) {
+        bits = torch_bits64(P, e0);
+        return e0 + 64 <= n ? bits : bits & ((1ull << (n - e0)) - 1ull);
+    }
     if (P.bits) {
         bits = P.bits[e0 >> 6];
         return e0 + 64 <= n ? bits : bits & ((1ull << (n - e0)) - 1ull);
@@ -793,6 +849,22 @@ static Pred make_pred(const void* mask, int mask_format, uint64_t seed, uint64_t
     Pred P;
     P.mask = mask_format == GA_MASK_BYTES ? (const uint8_t*)mask : nullptr;
     P.bits = mask_format == GA_MASK_BITS ? (const uint64_t*)mask : nullptr;
+    P.ttab = nullptr;
+    P.tn = 0;
+    P.tp = 0.f;
+    P.toff0 = P.tstep = 0;
+    P.tseedoff = nullptr;
+    P.tkey = make_uint2(0u, 0u);
+    if (mask_format == GA_MASK_TORCH && mask) {
+        const ga_sparta_torch_draw* d = (const ga_sparta_torch_draw*)mask;
+        P.ttab = d->table;
+        P.tn = d->ntens;
+        P.tp = d->p;
+        P.toff0 = d->offset0;
+        P.tstep = d->offset_step;
+        P.tseedoff = d->seedoff;
+        P.tkey = make_uint2((uint32_t)d->seed, (uint32_t)(d->seed >> 32));
+    }
     P.key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
     P.it_lo = (uint32_t)iteration;
     P.it_hi = (uint32_t)(iteration >> 32);
@@ -814,9 +886,14 @@ extern "C" GA_API int ga_sparta_select(int dtype, const void* src, int64_t K, in
     GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_select: bad layout %d", layout);
     GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_select: ld too small");
     GA_REQUIRE(p >= 0.0 && p <= 1.0, "ga_sparta_select: p=%g outside [0, 1]", p);
-    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS, "ga_sparta_select: bad mask_format %d",
-               mask_format);
-    GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_select: mask must be 16-byte aligned");
+    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS || mask_format == GA_MASK_TORCH,
+               "ga_sparta_select: bad mask_format %d", mask_format);
+    GA_REQUIRE(mask == nullptr || mask_format == GA_MASK_TORCH || ((uintptr_t)mask % 16) == 0,
+               "ga_sparta_select: mask must be 16-byte aligned");
+    GA_REQUIRE(mask_format != GA_MASK_TORCH || (mask && ((const ga_sparta_torch_draw*)mask)->table &&
+                                                ((const ga_sparta_torch_draw*)mask)->ntens > 0 &&
+                                                ((const ga_sparta_torch_draw*)mask)->offset0 % 4 == 0),
+               "ga_sparta_select: bad ga_sparta_torch_draw");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_select: bad skip table");
     if (n == 0) return hipMemsetAsync(count, 0, 2 * sizeof(int64_t), stream) == hipSuccess ? GA_OK : GA_EHIP;
     GA_REQUIRE(src && idx && vals, "ga_sparta_select: null src/idx/vals");
@@ -843,9 +920,14 @@ extern "C" GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, 
     GA_REQUIRE(layout == GA_LAYOUT_ROWS || layout == GA_LAYOUT_ELEM_MAJOR, "ga_sparta_average_local: bad layout");
     GA_REQUIRE(layout == GA_LAYOUT_ELEM_MAJOR ? ld >= K : (K == 1 || ld >= n), "ga_sparta_average_local: ld too small");
     GA_REQUIRE(p >= 0.0 && p <= 1.0, "ga_sparta_average_local: p=%g outside [0, 1]", p);
-    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS,
+    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS || mask_format == GA_MASK_TORCH,
                "ga_sparta_average_local: bad mask_format %d", mask_format);
-    GA_REQUIRE(mask == nullptr || ((uintptr_t)mask % 16) == 0, "ga_sparta_average_local: mask alignment");
+    GA_REQUIRE(mask == nullptr || mask_format == GA_MASK_TORCH || ((uintptr_t)mask % 16) == 0,
+               "ga_sparta_average_local: mask alignment");
+    GA_REQUIRE(mask_format != GA_MASK_TORCH || (mask && ((const ga_sparta_torch_draw*)mask)->table &&
+                                                ((const ga_sparta_torch_draw*)mask)->ntens > 0 &&
+                                                ((const ga_sparta_torch_draw*)mask)->offset0 % 4 == 0),
+               "ga_sparta_average_local: bad ga_sparta_torch_draw");
     GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_sparta_average_local: bad skip table");
     GA_REQUIRE((idx == nullptr && vals == nullptr && count == nullptr) || (idx && vals && count && work),
                "ga_sparta_average_local: idx, vals, count and work go together");
@@ -876,6 +958,8 @@ extern "C" GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64
 }
 
 extern "C" GA_API int64_t ga_sparta_torch_bernoulli_span(void) { return kTbSpan; }
+
+extern "C" GA_API int ga_sparta_torch_draw_bytes(void) { return (int)sizeof(ga_sparta_torch_draw); }
 
 extern "C" GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_t nblocks, float p,
                                                 uint64_t seed, uint64_t offset0, uint64_t offset_step,

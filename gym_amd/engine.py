@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import ops
+from .ops import TorchDraw
 from .comm import DONE, Collective
 from .demo_codec import DemoPlan
 
@@ -288,6 +289,11 @@ class Sparta:
         broadcast."""
         n = self.n
         cnt = None
+        if isinstance(mask, TorchDraw):  # the reference draw, computed inside the average kernel
+            if self.coll.exchange:
+                raise ValueError("Sparta: an in-kernel reference draw needs a local (no-exchange) step")
+            ops.sparta_average_local(reps, n, float(self.K_total), mask=mask, layout=self.layout)
+            return
         if mask is not None and mask.dtype == torch.int64:  # already packed (the fused reference draw)
             if mask_cap is None:
                 raise ValueError("Sparta: a packed mask needs mask_cap")

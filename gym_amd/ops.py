@@ -166,11 +166,32 @@ def sparta_torch_bernoulli(table, nblocks, p, seed, offset0, offset_step, mask, 
                                           _stream()), "ga_sparta_torch_bernoulli")
 
 
+class TorchDraw:
+    """The reference's mask draw described for the SPARTA kernels to compute
+    in-kernel (GA_MASK_TORCH): the table of sparta_bernoulli_table, p, the
+    generator state of the first drawn tensor (or a device {seed, offset}
+    tensor), the offset step per tensor."""
+
+    def __init__(self, table, p, seed, offset0, offset_step, seedoff=None):
+        self.table, self.p, self.seed, self.offset0 = table, float(p), int(seed), int(offset0)
+        self.offset_step, self.seedoff = int(offset_step), seedoff
+
+    def struct(self):
+        return _lib.TorchDraw(table=_p(self.table), ntens=int(self.table.shape[0]), p=self.p,
+                              seed=self.seed & (2**64 - 1), offset0=self.offset0, offset_step=self.offset_step,
+                              seedoff=_p(self.seedoff))
+
+
 def _mask_arg(mask, n, who):
-    """(mask, format code) of a SPARTA mask: uint8/bool per element, or int64
-    packed words (sparta_pack_mask)."""
+    """(mask, format code) of a SPARTA mask: uint8/bool per element, int64
+    packed words (sparta_pack_mask), or a TorchDraw (drawn in-kernel).  For a
+    TorchDraw the returned object is the ctypes struct (kept alive by the
+    caller for the call)."""
     if mask is None:
         return None, _lib.GA_MASK_BYTES
+    if isinstance(mask, TorchDraw):
+        _gpu(mask.table, mask.seedoff)
+        return mask.struct(), _lib.GA_MASK_TORCH
     if mask.dtype in (torch.uint8, torch.bool):
         if mask.numel() < n:
             raise ValueError(f"{who}: mask must have >= n elements")
@@ -180,6 +201,12 @@ def _mask_arg(mask, n, who):
             raise ValueError(f"{who}: packed mask must have >= ceil(n/64) words")
         return mask, _lib.GA_MASK_BITS
     raise ValueError(f"{who}: mask must be uint8/bool (per element) or int64 (packed words)")
+
+
+def _mptr(mask):
+    if isinstance(mask, ctypes.Structure):
+        return ctypes.addressof(mask)
+    return _p(mask)
 
 
 def sparta_workspace(n, device):
@@ -220,7 +247,7 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
     """Compact the selected elements of [0, n) (mask != 0, or the Philox draw
     outside the `skip` ranges) into idx (int32) and vals (= sum over the
     replicas of src); count[0] = number selected, count[1] = overflow flag."""
-    _gpu(src, idx, vals, count, work, mask, skip)
+    _gpu(src, idx, vals, count, work, None if isinstance(mask, TorchDraw) else mask, skip)
     src2, K, ld, code = _sparta_set(src, layout)
     if _rows_of(src2, code) < n:
         raise ValueError("sparta_select: replica set shorter than n")
@@ -233,7 +260,7 @@ def sparta_select(src, n, cap, idx, vals, count, work, mask=None, seed=0, iterat
         raise ValueError("sparta_select: workspace too small")
     mask, mfmt = _mask_arg(mask, n, "sparta_select")
     thr = _rate(p, mask)
-    check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, code, int(n), _p(mask), mfmt,
+    check(lib().ga_sparta_select(_dtype_code(src2), _p(src2), K, ld, code, int(n), _mptr(mask), mfmt,
                                  int(seed) & (2**64 - 1),
                                  int(iteration) & (2**64 - 1), thr, _p(skip), nskip, int(cap), _p(idx), _p(vals),
                                  _p(count),
@@ -245,7 +272,7 @@ def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0
     """Single-process SPARTA step over a replica set ([K, ld] rows, or [n, K]
     element-major): selected elements of every replica <- (sum over replicas)
     / divisor, one pass (optional packed idx/vals/count outputs as sparta_select)."""
-    _gpu(reps, mask, idx, vals, count, work, skip)
+    _gpu(reps, None if isinstance(mask, TorchDraw) else mask, idx, vals, count, work, skip)
     r2, K, ld, code = _sparta_set(reps, layout)
     if _rows_of(r2, code) < n:
         raise ValueError("sparta_average_local: replica set shorter than n")
@@ -257,7 +284,7 @@ def sparta_average_local(reps, n, divisor, mask=None, seed=0, iteration=0, p=0.0
         if idx.numel() < cap or vals.numel() < cap or work.numel() < lib().ga_sparta_workspace_bytes(int(n)):
             raise ValueError("sparta_average_local: output buffers too small")
     thr = _rate(p, mask)
-    check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, code, int(n), _p(mask), mfmt,
+    check(lib().ga_sparta_average_local(_dtype_code(r2), _p(r2), K, ld, code, int(n), _mptr(mask), mfmt,
                                         int(seed) & (2**64 - 1),
                                         int(iteration) & (2**64 - 1), thr, _p(skip), nskip, float(divisor),
                                         _p(idx), _p(vals),

@@ -211,7 +211,7 @@ class ReplicaRunner:
         process's and broadcasts it to the others."""
         a0 = self.ra.arenas[0]
         packed = draw_masks(self.s.index_selector, a0.params, self.ra.layout.views(self.mask), set(self._grad_less()),
-                            self.iteration, self.draw, bits=self.bits, coll=self.coll)
+                            self.iteration, self.draw, bits=self.bits, coll=self.coll, defer=True)
         self.mask_shared = packed is not None
         return self.mask if packed is None else packed
 

@@ -80,7 +80,7 @@ class MaskDraw:
         self.table = None
 
 
-def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=None):
+def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=None, defer=False):
     """Every tensor's selector mask into its view of a uint8 mask arena, in
     parameter order (sparta.py:28-33); tensors in `skip` stay 0.  Returns the
     mask to select with: `bits` (int64 packed words of the same arena,
@@ -91,6 +91,9 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
     already rank 0's on every rank (the reference broadcasts the masks,
     sparta.py:32-37); every rank's own generator still advances as its own
     draws would advance it.
+    defer (no exchange): the fused path returns an ops.TorchDraw instead of
+    drawing -- the SPARTA kernel then draws the same masks in-kernel
+    (GA_MASK_TORCH); the generator is advanced here all the same.
 
     RandomIndexSelector on a GPU: one ga_sparta_torch_bernoulli launch draws
     every tensor's mask exactly as the per-tensor torch.bernoulli calls would
@@ -129,7 +132,7 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
     on_gpu = bool(params) and params[0].device.type == "cuda"
     # inside a user's graph capture the generator offsets are graph-relative: torch's own kernels then
     if on_gpu and MaskDraw.fused and not torch.cuda.is_current_stream_capturing():
-        out = _draw_fused(selector, params, views, skip, state, bits, coll)
+        out = _draw_fused(selector, params, views, skip, state, bits, coll, defer)
         state.calls += 1
         return out
     for i, p in enumerate(params):
@@ -153,7 +156,7 @@ def _i64(v):
     return v - 2**64 if v >= 2**63 else v
 
 
-def _draw_fused(selector, params, views, skip, state, bits=None, coll=None):
+def _draw_fused(selector, params, views, skip, state, bits=None, coll=None, defer=False):
     """Every drawn tensor's torch.bernoulli(torch.full(shape, p)) in ONE launch
     (ga_sparta_torch_bernoulli: ATen's HIP kernel for it restated, bit for
     bit), with the default generator of the device read and advanced exactly
@@ -172,6 +175,13 @@ def _draw_fused(selector, params, views, skip, state, bits=None, coll=None):
         state.skip_words = [((views[i].storage_offset() - base.storage_offset()) // 64,
                              -(-(views[i].storage_offset() - base.storage_offset() + views[i].numel()) // 64))
                             for i in sorted(skip)]
+    table, nblocks = state.table
+    dev = state.base.device
+    gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+    if defer and not (coll is not None and coll.exchange) and state.ndrawn > 0:
+        off0 = gen.get_offset()
+        gen.set_offset(off0 + MaskDraw.offset_step * state.ndrawn)
+        return ops.TorchDraw(table, selector.p, gen.initial_seed(), off0, MaskDraw.offset_step)
     out = state.base
     if bits is not None:
         if bits.dtype != torch.int64 or bits.numel() < ops.sparta_mask_words(state.base.numel()):
@@ -182,9 +192,6 @@ def _draw_fused(selector, params, views, skip, state, bits=None, coll=None):
     else:
         for i in skip:
             views[i].zero_()
-    table, nblocks = state.table
-    dev = state.base.device
-    gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
     off0 = gen.get_offset()
     seedoff = None
     if coll is not None and coll.exchange:  # rank 0's generator state, 16 bytes on the wire

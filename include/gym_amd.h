@@ -54,6 +54,19 @@ extern "C" {
  *   GA_MASK_BITS   uint64 words, bit j of word w = element 64 w + j (ga_sparta_pack_mask) */
 #define GA_MASK_BYTES 0
 #define GA_MASK_BITS 1
+#define GA_MASK_TORCH 2
+
+/* GA_MASK_TORCH: the mask argument points to this HOST struct, and the select /
+ * average kernels draw the reference's masks themselves, exactly as
+ * ga_sparta_torch_bernoulli would write them (no mask in memory). */
+typedef struct ga_sparta_torch_draw {
+    const int64_t* table;     /* device rows {arena offset (multiple of 64), numel, -} per drawn tensor, ascending */
+    int32_t ntens;            /* rows */
+    float p;                  /* selection probability as torch.full(shape, p) holds it (fp32) */
+    uint64_t seed, offset0;   /* torch generator state for the first drawn tensor */
+    uint64_t offset_step;     /* generator offset per tensor (12) */
+    const uint64_t* seedoff;  /* device {seed, offset0} overriding the two above, or null */
+} ga_sparta_torch_draw;
 
 /* ---- library ---------------------------------------------------------- */
 
@@ -155,6 +168,9 @@ GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64_t* bits, h
  * broadcasts the masks themselves, sparta.py:32-37).  The caller advances its
  * torch generator by ntens * offset_step.
  */
+/* sizeof(ga_sparta_torch_draw) (binding layout check). */
+GA_API int ga_sparta_torch_draw_bytes(void);
+
 /* Elements per workgroup of ga_sparta_torch_bernoulli (the table's first-workgroup unit). */
 GA_API int64_t ga_sparta_torch_bernoulli_span(void);
 
@@ -170,7 +186,9 @@ GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t ntens, int64_
  *   mask source: if mask != null, element i is selected iff its mask entry is
  *   set (mask_format GA_MASK_BYTES: uint8 mask arena, GA_MASK_BITS: the packed
  *   words of ga_sparta_pack_mask -- rank 0's per-tensor index_selector masks,
- *   broadcast, sparta.py:32-37); otherwise the in-kernel Philox4x32-10 stream decides
+ *   broadcast, sparta.py:32-37; GA_MASK_TORCH: mask -> a host
+ *   ga_sparta_torch_draw, the reference's draw computed in-kernel); otherwise
+ *   the in-kernel Philox4x32-10 stream decides
  *   with selection rate p (see ga_sparta_gap_table), except inside the `nskip` element ranges skip[2r] <= i < skip[2r+1]
  *   (sorted, disjoint: the tensors without a gradient, which the reference
  *   skips, sparta.py:29-30; skip may be null when nskip == 0).

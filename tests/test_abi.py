@@ -20,8 +20,9 @@ def test_exports_every_header_symbol():
 
 def test_version_and_struct_layout():
     L = _lib.lib()
-    assert L.ga_abi_version() == 102
+    assert L.ga_abi_version() == 103
     assert L.ga_demo_tensor_bytes() == ctypes.sizeof(_lib.DemoTensor) == 56
+    assert L.ga_sparta_torch_draw_bytes() == ctypes.sizeof(_lib.TorchDraw) == 48
 
 
 def test_sparta_gap_table_and_workspace():
@@ -42,6 +43,9 @@ def test_sparta_gap_table_and_workspace():
     assert L.ga_sparta_workspace_bytes(16384 * 10) >= 2 * 4 * 10
 
 
+_NULL_TABLE_DRAW = _lib.TorchDraw(table=None, ntens=1, p=0.5, seed=1, offset0=0, offset_step=12, seedoff=None)
+
+
 @pytest.mark.parametrize("call", [
     lambda L: L.ga_replica_mean(0, None, 1, 8, None, 8, 1.0, None, 1, 8, None),
     lambda L: L.ga_replica_mean(7, ctypes.c_void_p(64), 1, 8, None, 8, 1.0, ctypes.c_void_p(64), 1, 8, None),
@@ -49,9 +53,12 @@ def test_sparta_gap_table_and_workspace():
     lambda L: L.ga_diloco_outer(0, ctypes.c_void_p(64), 1, 8, 8, 1.0, ctypes.c_void_p(64), None, 1, 0, 0.7, 0.9,
                                 0.0, 0.0, 1, ctypes.c_void_p(64), 1, 8, None),
     lambda L: L.ga_sparta_select(0, None, 1, 8, 0, 8, None, 0, 1, 1, 10, None, 0, 8, None, None, None, None, None),
-    lambda L: L.ga_sparta_select(0, ctypes.c_void_p(64), 1, 8, 0, 8, ctypes.c_void_p(64), 2, 1, 1, 0.5, None, 0, 8,
+    lambda L: L.ga_sparta_select(0, ctypes.c_void_p(64), 1, 8, 0, 8, ctypes.c_void_p(64), 3, 1, 1, 0.5, None, 0, 8,
                                  ctypes.c_void_p(64), ctypes.c_void_p(64), ctypes.c_void_p(64), ctypes.c_void_p(64),
                                  None),
+    lambda L: L.ga_sparta_average_local(0, ctypes.c_void_p(64), 1, 8, 0, 8,
+                                        ctypes.addressof(_NULL_TABLE_DRAW), 2, 1, 1, 0.5, None, 0, 1.0,
+                                        None, None, 0, None, None, None),
     lambda L: L.ga_sparta_pack_mask(ctypes.c_void_p(64), 100, None, None),
     lambda L: L.ga_sparta_pack_mask(ctypes.c_void_p(65), 100, ctypes.c_void_p(64), None),
     lambda L: L.ga_demo_encode(0, None, 0, 0, None, None, None, None, None, 1, 8, 0.1, 0.9, 1.0, None, 0, 0, None),

@@ -960,3 +960,49 @@ def test_torch_gpu_bernoulli_oracle_and_kernel(numel, p):
     gb = bits.cpu().numpy()
     assert gb[0] == -1 and all(gb[w] == -1 for w in range(1 + -(-numel // 64), words))
     assert np.array_equal(gb[1:1 + -(-numel // 64)], osparta.pack_mask(want))
+
+
+@pytest.mark.parametrize("layout,K", [("elem", 32), ("rows", 3)])
+def test_sparta_in_kernel_reference_draw(layout, K):
+    """GA_MASK_TORCH: the average kernel draws the reference's masks itself
+    (draw_masks(defer=True) -> ops.TorchDraw) -- the same averages as with the
+    fused draw's packed mask and the oracle's restatement of torch's stream,
+    and the generator advanced identically; a grad-less tensor is skipped and
+    tensor ends fall inside 64-element groups."""
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.strategy.sparta import MaskDraw, RandomIndexSelector, draw_masks
+    shapes = [(300, 77), (768,), (5, 9), (1000, 64), (3,)]
+    L = ArenaLayout(shapes)
+    params = [torch.zeros(s, device=DEV) for s in shapes]
+    sel = RandomIndexSelector(0.05)
+    skip = {2}
+    rng = np.random.default_rng(K)
+    x = rng.standard_normal((K, L.n)).astype(np.float32)
+    mk = (lambda a: t(np.ascontiguousarray(a.T))) if layout == "elem" else t
+    mask = torch.zeros(L.n, dtype=torch.uint8, device=DEV)
+    outs, gens = [], []
+    for defer in (False, True):
+        torch.manual_seed(99)
+        torch.rand(7, device=DEV)
+        gen = torch.cuda.default_generators[0]
+        seed, off0 = gen.initial_seed(), gen.get_offset()
+        bits = torch.zeros(ops.sparta_mask_words(L.n), dtype=torch.int64, device=DEV)
+        m = draw_masks(sel, params, L.views(mask), skip, 0, MaskDraw(), bits=bits, defer=defer)
+        assert isinstance(m, ops.TorchDraw) == defer
+        gens.append(torch.cuda.get_rng_state())
+        src = mk(x)
+        ops.sparta_average_local(src, L.n, float(K), mask=m, layout=layout)
+        outs.append(host(src).T if layout == "elem" else host(src))
+    assert torch.equal(gens[0], gens[1])
+    # the oracle: torch's stream per drawn tensor, offset + 12 per tensor
+    want_mask = np.zeros(L.n, bool)
+    i = 0
+    for j, (o, nn) in enumerate(zip(L.offsets, L.numels)):
+        if j in skip:
+            continue
+        want_mask[o:o + nn] = osparta.torch_gpu_bernoulli(nn, 0.05, seed, off0 + 12 * i)
+        i += 1
+    want = osparta.sparse_average(list(x), want_mask)
+    for k in range(K):
+        assert np.array_equal(outs[0][k], want[k]) and np.array_equal(outs[1][k], want[k]), k
