@@ -8,6 +8,8 @@ Modes (BASELINE configs):
   demo_decode8  ga_demo_decode_sym, 8 distinct gathered payloads (what every GPU runs at 8 nodes)
   sparta_elem   ga_sparta_average_local, K=32 GPT-2 124M, [n, K] element-major (configs[3])
   sparta_rows   the same on the [K, n] row layout
+  sparta_torch  the same [n, K] step with the reference's torch.bernoulli stream drawn in-kernel (GA_MASK_TORCH)
+  torch_draw    ga_sparta_torch_bernoulli: the reference's per-tensor draws for GPT-2 124M as one packed mask
   diloco        ga_diloco_outer, K=8 GPT-2 124M (configs[2])
 Prints the HIP-event mean per launch and the algorithmic bytes per launch as one JSON line.
 Usage: python tools/prof_kernels.py <mode> [launches]"""
@@ -81,6 +83,30 @@ def main():
             P.copy_(P0)
             alg = 12 * n + 8 * plan.M * S
         out.update(model="gpt2-350m", n=n, M=plan.M)
+    elif mode in ("sparta_torch", "torch_draw"):
+        layout = ArenaLayout(MODELS["gpt2-124m"]())
+        K, p = 32, 0.005
+        table, nblocks = ops.sparta_bernoulli_table(layout.offsets, layout.numels, dev)
+        off = [0]
+        if mode == "torch_draw":
+            bits = torch.zeros(ops.sparta_mask_words(layout.n), dtype=torch.int64, device=dev)
+
+            def step():
+                ops.sparta_torch_bernoulli(table, nblocks, p, 1234, off[0], 12, bits)
+                off[0] += 12 * len(layout.numels)
+
+            alg = ops.sparta_mask_words(layout.n) * 8
+        else:
+            reps = synth(layout, K, dev).t().contiguous()
+
+            def step():
+                ops.sparta_average_local(reps, layout.n, float(K), mask=ops.TorchDraw(table, p, 1234, off[0], 12),
+                                         layout="elem")
+                off[0] += 12 * len(layout.numels)
+
+            alg = 2 * 4 * K * int(round(layout.n * p))
+        ms = timed(step, launches)
+        out.update(model="gpt2-124m", K=K, p=p, tensors=len(layout.numels))
     elif mode.startswith("sparta"):
         layout = ArenaLayout(MODELS["gpt2-124m"]())
         K, p = 32, 0.005
