@@ -102,12 +102,18 @@ __device__ __forceinline__ int gap_of(const uint64_t* tab, uint32_t u) {
 // (tensor offsets are multiples of 64, so the group lies in one tensor or in
 // padding / a tensor not drawn): 16 Philox calls, four chains at a time
 __device__ __forceinline__ uint64_t torch_bits64(const Pred& P, int64_t e0) {
+    // last drawn tensor starting at or before e0: a wave-uniform (scalar) search
+    // for the wave's first active lane, then each lane walks forward (lanes hold
+    // increasing e0 in every caller; a 64-group tile spans few tensors)
+    const int64_t ef = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(e0 >> 32)) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)e0));
     int lo = 0, hi = P.tn - 1;
-    while (lo < hi) {  // last drawn tensor starting at or before e0
+    while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (P.ttab[3 * mid] <= e0) lo = mid;
+        if (P.ttab[3 * mid] <= ef) lo = mid;
         else hi = mid - 1;
     }
+    while (lo + 1 < P.tn && P.ttab[3 * (lo + 1)] <= e0) ++lo;
     const int64_t base = P.ttab[3 * lo], numel = P.ttab[3 * lo + 1];
     if (e0 < base || e0 >= base + numel) return 0ull;
     uint2 key = P.tkey;
