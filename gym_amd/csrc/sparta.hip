@@ -509,11 +509,12 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
 // mixes waves drawing their mask with waves whose gathers are in flight.  The
 // wave scans its lanes' selection counts with shuffles, lists the selected
 // positions in its own LDS, then moves each element's K values as KQ lanes x
-// one 4-replica vector (whole 128-B lines at K = 32 fp32), up to 4 passes of
-// loads in flight per lane, stages them at an odd LDS stride, sums each element
-// in ascending replica order and divides (the tile-gather kernel's fp32 order:
+// one 4-replica vector (whole 128-B lines at K = 32 fp32), up to 8 passes of
+// loads in flight per lane, sums each element in ascending replica order across
+// its lanes in registers and divides (the tile-gather kernel's fp32 order:
 // bit-identical), and writes the average back to every replica.
-// Measured (K = 32, 124M, p = 0.005): 0.049-0.053 ms against 0.054-0.063 ms for
+// Measured (K = 32, 124M, p = 0.005): 0.049-0.053 ms (0.047-0.052 with the
+// register-only batch) against 0.054-0.063 ms for
 // the 16384-element tile-gather kernel; a persistent form that draws tile t+1's
 // mask while tile t's loads are in flight ran 0.062 / 0.065 / 0.074 ms at 2 / 4 /
 // 8 tiles per wave (fewer waves in flight), and builds of the kernel with only
@@ -531,63 +532,65 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One batch (<= EB listed elements from list[b0]): loads, LDS staging, ascending
-// replica sums, divide, write-back.
+// One batch (<= EB listed elements from list[b0]) in registers: each element's K
+// values stay in its KQ lanes (4 per lane) and the ascending-replica sum walks
+// the lanes with DPP row shifts (lane q adds its four values to lane q - 1's
+// running sum: the oracle's sequential order exactly), then the last lane's
+// average is broadcast back.  No LDS staging, no wave_sync; NP passes (8
+// elements each at K = 32) in flight.  An LDS-staged form (values written at an
+// odd stride, summed by one lane per element) measured 5% slower
+// (profiles/r02x_ab_sparta_batch.txt).
+#ifndef GA_SP_DPP_PASSES
+#define GA_SP_DPP_PASSES 8
+#endif
 template <typename T, int KQ>
-struct WaveBatch {
-    static constexpr int K = 4 * KQ, Kp = K + 1, EPP = 64 / KQ, EB = 4 * EPP;
+struct WaveBatchDpp {
+    static constexpr int K = 4 * KQ, EPP = 64 / KQ, NP = GA_SP_DPP_PASSES, EB = NP * EPP;
     using V = typename Vec4<T>::type;
-    __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0, int ne,
-                                               int lane, float* stage, float divisor) {
+    __device__ __forceinline__ static float shr1(float a) {  // lane i <- lane i - 1 within each 16-lane row
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x111, 0xf, 0xf, true));
+    }
+    __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0,
+                                               int ne, int lane, float divisor) {
         const int q = lane % KQ, el = lane / KQ;
-        V v[4];
+        V v[NP];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NP; ++u) {
             const int e = u * EPP + el;
             if (e < ne) v[u] = *reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NP; ++u) {
+            if (u * EPP >= ne) break;  // wave-uniform
             const int e = u * EPP + el;
-            if (e < ne) {
-                float f[4];
-                Vec4<T>::unpack(v[u], f);
+            float f[4] = {0.f, 0.f, 0.f, 0.f};
+            if (e < ne) Vec4<T>::unpack(v[u], f);
+            float a = 0.f;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) stage[e * Kp + 4 * q + r] = f[r];
+            for (int s = 0; s < KQ; ++s) {
+                float left = KQ > 1 ? shr1(a) : 0.f;
+                if (q == 0) left = 0.f;
+                const float c = (((left + f[0]) + f[1]) + f[2]) + f[3];
+                a = q == s ? c : a;
             }
-        }
-        wave_sync();
-        for (int e = lane; e < ne; e += 64) {
-            float acc = 0.f;
-#pragma unroll
-            for (int k = 0; k < K; ++k) acc += stage[e * Kp + k];
-            stage[e * Kp] = acc / divisor;
-        }
-        wave_sync();
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e = u * EPP + el;
+            const float avg = __shfl(a / divisor, (lane & ~(KQ - 1)) | (KQ - 1), 64);
             if (e < ne) {
-                const float a = stage[e * Kp];
-                const float w[4] = {a, a, a, a};
+                const float w[4] = {avg, avg, avg, avg};
                 *reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q) = Vec4<T>::pack(w);
             }
         }
-        wave_sync();
     }
 };
 
 template <typename T, int KQ>
 __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(Pred P, int64_t n, T* __restrict__ src,
                                                                                int64_t ld, float divisor) {
-    using B = WaveBatch<T, KQ>;
+    using B = WaveBatchDpp<T, KQ>;
     __shared__ uint64_t tab[kGapTable];
     __shared__ uint16_t lists[GA_SP_WAVES][kWList];
-    __shared__ float stages[GA_SP_WAVES][B::EB * B::Kp];
     load_gap_table(P, tab);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint16_t* list = lists[wid];
-    float* stage = stages[wid];
     const int64_t t = (int64_t)blockIdx.x * GA_SP_WAVES + wid;
     const int64_t tile0 = t * kWTile;
     const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
@@ -615,7 +618,7 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(P
         wave_sync();
         const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
         for (int b0 = 0; b0 < wtot; b0 += B::EB)
-            B::run(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, stage, divisor);
+            B::run(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, divisor);
     }
 }
 
