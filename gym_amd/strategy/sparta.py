@@ -131,7 +131,8 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
 
     on_gpu = bool(params) and params[0].device.type == "cuda"
     # inside a user's graph capture the generator offsets are graph-relative: torch's own kernels then
-    if on_gpu and MaskDraw.fused and not torch.cuda.is_current_stream_capturing():
+    if (on_gpu and MaskDraw.fused and not torch.cuda.is_current_stream_capturing()
+            and fused_draw_matches_torch(params[0].device)):
         out = _draw_fused(selector, params, views, skip, state, bits, coll, defer)
         state.calls += 1
         return out
@@ -149,6 +150,41 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
     else:
         body()
     state.calls += 1
+
+
+_FUSED_OK = {}
+
+
+def fused_draw_matches_torch(device):
+    """One-time check per device that ga_sparta_torch_bernoulli still restates
+    this torch build's bernoulli kernel: a 3-tensor probe drawn both ways from
+    the same generator state (bits, and the state torch leaves behind), the
+    caller's generator state restored afterwards.  False -> draw_masks uses
+    torch's own kernels."""
+    key = str(device)
+    if key not in _FUSED_OK:
+        dev = torch.device(device)
+        gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+        state = torch.cuda.get_rng_state(dev)
+        try:
+            shapes = [(4099,), (64, 65), (1,)]
+            p = 0.3
+            want = [torch.bernoulli(torch.full(s, p, device=dev)).bool().reshape(-1) for s in shapes]
+            after = torch.cuda.get_rng_state(dev)
+            torch.cuda.set_rng_state(state, dev)
+            numels = [w.numel() for w in want]
+            offs = [sum(-(-m // 64) * 64 for m in numels[:i]) for i in range(len(numels))]
+            table, nb = ops.sparta_bernoulli_table(offs, numels, dev)
+            mask = torch.zeros(offs[-1] + numels[-1], dtype=torch.uint8, device=dev)
+            off0 = gen.get_offset()
+            ops.sparta_torch_bernoulli(table, nb, p, gen.initial_seed(), off0, MaskDraw.offset_step, mask)
+            same_bits = all(torch.equal(mask[a:a + m].bool(), w) for a, m, w in zip(offs, numels, want))
+            gen.set_offset(off0 + MaskDraw.offset_step * len(shapes))
+            same_state = torch.equal(torch.cuda.get_rng_state(dev), after)
+            _FUSED_OK[key] = bool(same_bits and same_state)
+        finally:
+            torch.cuda.set_rng_state(state, dev)
+    return _FUSED_OK[key]
 
 
 def _i64(v):

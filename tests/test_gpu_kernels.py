@@ -1006,3 +1006,14 @@ def test_sparta_in_kernel_reference_draw(layout, K):
     want = osparta.sparse_average(list(x), want_mask)
     for k in range(K):
         assert np.array_equal(outs[0][k], want[k]) and np.array_equal(outs[1][k], want[k]), k
+
+
+def test_fused_draw_self_check():
+    """The one-time probe draw_masks runs before using the fused draw agrees
+    with this torch build (and leaves the caller's generator untouched)."""
+    from gym_amd.strategy import sparta as sp
+    sp._FUSED_OK.clear()
+    torch.manual_seed(5)
+    before = torch.cuda.get_rng_state()
+    assert sp.fused_draw_matches_torch(DEV)
+    assert torch.equal(torch.cuda.get_rng_state(), before)
