@@ -519,7 +519,11 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
 // mask while tile t's loads are in flight ran 0.062 / 0.065 / 0.074 ms at 2 / 4 /
 // 8 tiles per wave (fewer waves in flight), and builds of the kernel with only
 // its mask (0.015 ms) or only its gather (0.034 ms) add up to the whole.
-constexpr int kWTile = 64 * kSpPerThread;  // elements per wavefront tile
+#ifndef GA_SP_GROUPS
+#define GA_SP_GROUPS 1  // 64-element groups per lane (2: no faster, profiles/r02x_ab_sparta_groups.txt)
+#endif
+constexpr int kWGroups = GA_SP_GROUPS;
+constexpr int kWTile = 64 * kSpPerThread * kWGroups;  // elements per wavefront tile
 constexpr int kWList = 256;                // listed positions per window
 #ifndef GA_SP_WAVES
 #define GA_SP_WAVES 4  // wavefronts (independent tiles) per workgroup
@@ -593,9 +597,16 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(P
     uint16_t* list = lists[wid];
     const int64_t t = (int64_t)blockIdx.x * GA_SP_WAVES + wid;
     const int64_t tile0 = t * kWTile;
-    const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
-    const uint64_t bits = e0 < n ? pred_bits64(P, tab, e0, n) : 0ull;
-    const int c = __popcll(bits);
+    // lane owns the kWGroups consecutive 64-element groups from e0 (ascending over lanes)
+    const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread * kWGroups;
+    uint64_t bits[kWGroups];
+    int c = 0;
+#pragma unroll
+    for (int g = 0; g < kWGroups; ++g) {
+        const int64_t eg = e0 + (int64_t)g * kSpPerThread;
+        bits[g] = eg < n ? pred_bits64(P, tab, eg, n) : 0ull;
+        c += __popcll(bits[g]);
+    }
     int x = c;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -606,13 +617,17 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(P
     const int local0 = x - c;
     for (int w0 = 0; w0 < total; w0 += kWList) {  // one window unless p is large
         {
-            uint64_t b = bits;
             int l = local0;
-            while (b) {
-                const int j = __builtin_ctzll(b);
-                b &= b - 1;
-                if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * kSpPerThread + j);
-                ++l;
+#pragma unroll
+            for (int g = 0; g < kWGroups; ++g) {
+                uint64_t b = bits[g];
+                while (b) {
+                    const int j = __builtin_ctzll(b);
+                    b &= b - 1;
+                    if (l >= w0 && l < w0 + kWList)
+                        list[l - w0] = (uint16_t)((lane * kWGroups + g) * kSpPerThread + j);
+                    ++l;
+                }
             }
         }
         wave_sync();
