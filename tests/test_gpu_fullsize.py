@@ -198,3 +198,49 @@ def test_demo_gpt2_350m_sampled_chunks():
         e0 += ne
     assert checked > 50
     tally.done()
+
+
+def test_sparta_reference_draw_gpt2_124m_32_nodes():
+    """The drop-in default SPARTA draw at configs[3]'s size: the average kernel
+    drawing torch.bernoulli's stream itself (GA_MASK_TORCH) and the fused draw's
+    packed mask select the same elements as the 148 per-tensor torch.bernoulli
+    calls on this GPU (the reference's draw, sparta.py:80-85), and the two
+    averages of the 32 nodes' [n, K] set are bit-identical."""
+    from gym_amd import ops
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.shapes import MODELS
+    from gym_amd.strategy.sparta import MaskDraw, RandomIndexSelector, draw_masks
+    L = ArenaLayout(MODELS["gpt2-124m"]())
+    K, p = 32, 0.005
+    params = L.views(torch.empty(L.n, device=DEV))
+    sel = RandomIndexSelector(p)
+    torch.manual_seed(2024)
+    gen0 = torch.cuda.get_rng_state()
+    want = torch.zeros(L.n, dtype=torch.bool, device=DEV)  # the reference's draws
+    for v, prm in zip(L.views(want), params):
+        v.copy_(sel.get_indices(prm, 0))
+    after = torch.cuda.get_rng_state()
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    em = torch.randn(L.n, K, device=DEV, generator=g)
+    outs = []
+    for defer in (True, False):
+        torch.cuda.set_rng_state(gen0)
+        mask = torch.zeros(L.n, dtype=torch.uint8, device=DEV)
+        bits = torch.zeros(ops.sparta_mask_words(L.n), dtype=torch.int64, device=DEV)
+        m = draw_masks(sel, params, L.views(mask), set(), 0, MaskDraw(), bits=bits, defer=defer)
+        assert torch.equal(torch.cuda.get_rng_state(), after)
+        if not defer:
+            got = torch.from_numpy(osparta.unpack_mask(m.cpu().numpy(), L.n)).to(DEV)
+            assert torch.equal(got, want)
+        x = em.clone()
+        ops.sparta_average_local(x, L.n, float(K), mask=m, layout="elem")
+        outs.append(x)
+    assert torch.equal(outs[0], outs[1])
+    sel_idx = want.nonzero().view(-1)
+    rest = ~want
+    assert torch.equal(outs[0][rest], em[rest])  # unselected elements untouched
+    i = sel_idx[:: max(1, sel_idx.numel() // 2000)]
+    exp = torch.from_numpy(np.stack([osparta.sparse_average(list(em[j].cpu().numpy().reshape(K, 1)),
+                                                            np.ones(1, bool))[0] for j in i.tolist()]).reshape(-1))
+    assert torch.equal(outs[0][i, 0].cpu(), exp)
