@@ -118,7 +118,9 @@ def main():
 
         def step():
             ops.sparta_average_local(reps, layout.n, float(K), seed=42, iteration=it[0], p=p, layout=kind)
-            it[0] += 1
+            # GA_PROF_FIXED_ITER=1: the same mask every launch (its lines stay in
+            # the Infinity Cache), as the fixed-position gather ubench
+            it[0] += 0 if os.environ.get("GA_PROF_FIXED_ITER") == "1" else 1
 
         ms = timed(step, launches)
         sel = int(round(layout.n * p))

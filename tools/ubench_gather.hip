@@ -167,6 +167,32 @@ int main() {
         repl(nm, time_ms([&] { read_lines_flat<<<g, 256>>>(a4, dpos, M, out); }, reps), 0);
     }
     repl("lines rmw 16384-tiles", time_ms([&] { rmw_lines_tiles<<<(unsigned)ts16.size() - 1, 256>>>(a4, dpos, dts16); }, reps), 1);
+    // The same kernel over NSETS independent position sets in rotation: a fixed
+    // set (80 MB of lines) stays in the 256 MiB Infinity Cache from launch to
+    // launch; four sets (320 MB) do not, as a SPARTA step whose mask changes
+    // every iteration does not.
+    const int NSETS = 4;
+    std::vector<int*> rpos(NSETS), rts(NSETS);
+    for (int s = 0; s < NSETS; ++s) {
+        std::mt19937_64 r2(1000 + s);
+        std::vector<int> ps;
+        std::vector<int> tt((n + 16383) / 16384 + 1, 0);
+        for (long i = 0; i < n; ++i) {
+            if (U(r2) < p) ps.push_back((int)i);
+            if ((i & 16383) == 16383 || i == n - 1) tt[i / 16384 + 1] = (int)ps.size();
+        }
+        CK(hipMalloc(&rpos[s], sizeof(int) * ps.size()));
+        CK(hipMalloc(&rts[s], sizeof(int) * tt.size()));
+        CK(hipMemcpy(rpos[s], ps.data(), sizeof(int) * ps.size(), hipMemcpyHostToDevice));
+        CK(hipMemcpy(rts[s], tt.data(), sizeof(int) * tt.size(), hipMemcpyHostToDevice));
+    }
+    int cur = 0;
+    const unsigned g16 = (unsigned)ts16.size() - 1;
+    repl("lines rmw 16384-tiles 1 set", time_ms([&] { rmw_lines_tiles<<<g16, 256>>>(a4, rpos[0], rts[0]); }, 4 * reps), 1);
+    repl("lines rmw 16384-tiles 4 sets", time_ms([&] {
+        rmw_lines_tiles<<<g16, 256>>>(a4, rpos[cur], rts[cur]);
+        cur = (cur + 1) % NSETS;
+    }, 4 * reps), 1);
     CK(hipFree(a));
     return 0;
 }
