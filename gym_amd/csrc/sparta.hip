@@ -57,7 +57,8 @@ struct Pred {
     const uint64_t* bits; // packed mask (bit j of word w = element 64 w + j), or null; both null -> Philox
     const int64_t* ttab;  // GA_MASK_TORCH: the reference draw in-kernel (ga_sparta_torch_draw), or null
     int32_t tn;
-    float tp;
+    uint32_t tthr;  // select a 32-bit Philox word w iff tany && w <= tthr (tb_threshold)
+    int32_t tany;
     uint64_t toff0, tstep;
     const uint64_t* tseedoff;
     uint2 tkey;
@@ -98,6 +99,38 @@ __device__ __forceinline__ int gap_of(const uint64_t* tab, uint32_t u) {
     return t;
 }
 
+// The 64-element word of torch's bernoulli stream at 4-element group t0 (t0 %
+// 16 == 0): 16 Philox calls with counter {ctr, t}, four independent chains at
+// a time; element 4t + j is selected iff word j of call t is <= thr (the exact
+// integer form of rocrand's uniform 2^-32 + w 2^-32 <= p, see tb_threshold),
+// and only the first `rem` elements exist.
+__device__ __forceinline__ uint64_t torch_word(uint2 key, uint64_t ctr, uint64_t t0, int64_t rem, uint32_t thr,
+                                               int32_t any) {
+    uint32_t half[2] = {0u, 0u};
+#pragma unroll
+    for (int c0 = 0; c0 < 16; c0 += 4) {
+        uint4 w[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint64_t t = t0 + c0 + c;
+            w[c] = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
+                                 key);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t ws[4] = {w[c].x, w[c].y, w[c].z, w[c].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int e = 4 * (c0 + c) + j;
+                half[e >> 5] |= (ws[j] <= thr ? 1u : 0u) << (e & 31);
+            }
+        }
+    }
+    const uint64_t bits = ((uint64_t)half[1] << 32) | half[0];
+    if (!any || rem <= 0) return 0ull;
+    return rem >= 64 ? bits : bits & ((1ull << rem) - 1ull);
+}
+
 // GA_MASK_TORCH: the 64 elements at e0 as ga_sparta_torch_bernoulli draws them
 // (tensor offsets are multiples of 64, so the group lies in one tensor or in
 // padding / a tensor not drawn): 16 Philox calls, four chains at a time
@@ -125,29 +158,7 @@ __device__ __forceinline__ uint64_t torch_bits64(const Pred& P, int64_t e0) {
     }
     const uint64_t ctr = (off0 + (uint64_t)lo * P.tstep) >> 2;
     const int64_t rel = e0 - base;
-    const uint64_t t0 = (uint64_t)rel >> 2;
-    const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
-    uint64_t bits = 0;
-#pragma unroll
-    for (int c0 = 0; c0 < 16; c0 += 4) {
-        uint4 w[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint64_t t = t0 + c0 + c;
-            w[c] = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
-                                 key);
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t ws[4] = {w[c].x, w[c].y, w[c].z, w[c].w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int e = 4 * (c0 + c) + j;
-                if (rel + e < numel && (inv + (float)ws[j] * inv) <= P.tp) bits |= 1ull << e;
-            }
-        }
-    }
-    return bits;
+    return torch_word(key, ctr, (uint64_t)rel >> 2, numel - rel, P.tthr, P.tany);
 }
 
 // Selection bits of the 64 elements starting at element `e0` (e0 % 64 == 0);
@@ -752,11 +763,14 @@ __global__ __launch_bounds__(kSpBlock) void sparta_pack_mask_kernel(const uint8_
 constexpr int kTbCalls = GA_TB_CALLS;                 // Philox calls (4-element groups) per lane
 constexpr int64_t kTbSpan = 4 * kSpBlock * kTbCalls;  // elements per workgroup
 
+// Packed output: one wavefront per workgroup span, each lane the 16 calls of
+// one 64-element word (no cross-lane assembly).
+constexpr int kTbWordLanes = (int)(kTbSpan / 64);
+
 template <bool BITS>
-__global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const int64_t* __restrict__ tab, int ntens,
-                                                                         float p, uint2 key, uint64_t off0,
-                                                                         uint64_t step, const uint64_t* seedoff,
-                                                                         void* __restrict__ mask) {
+__global__ __launch_bounds__(BITS ? kTbWordLanes : kSpBlock) void sparta_torch_bernoulli_kernel(
+    const int64_t* __restrict__ tab, int ntens, uint32_t thr, int32_t any, uint2 key, uint64_t off0, uint64_t step,
+    const uint64_t* seedoff, void* __restrict__ mask) {
     if (seedoff) {  // the generator state as rank 0 broadcast it (device memory)
         const uint64_t sd = seedoff[0];
         key = make_uint2((uint32_t)sd, (uint32_t)(sd >> 32));
@@ -770,9 +784,15 @@ __global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const 
         else hi = mid - 1;
     }
     const int64_t base = tab[3 * lo], numel = tab[3 * lo + 1];
-    const uint64_t t0 = (uint64_t)(b - tab[3 * lo + 2]) * kSpBlock * kTbCalls + threadIdx.x;
     const uint64_t ctr = (off0 + (uint64_t)lo * step) >> 2;
-    const float inv = 2.3283064e-10f;  // 2^-32 (rocrand uniform: (0, 1])
+    if constexpr (BITS) {
+        const int64_t rel = (int64_t)(b - tab[3 * lo + 2]) * kTbSpan + 64 * (int64_t)threadIdx.x;
+        if (rel < numel)
+            reinterpret_cast<uint64_t*>(mask)[(base + rel) >> 6] =
+                torch_word(key, ctr, (uint64_t)rel >> 2, numel - rel, thr, any);
+        return;
+    }
+    const uint64_t t0 = (uint64_t)(b - tab[3 * lo + 2]) * kSpBlock * kTbCalls + threadIdx.x;
     uint4 w[kTbCalls];
 #pragma unroll
     for (int c = 0; c < kTbCalls; ++c) {  // independent chains: the calls interleave
@@ -785,20 +805,8 @@ __global__ __launch_bounds__(kSpBlock) void sparta_torch_bernoulli_kernel(const 
         const uint32_t ws[4] = {w[c].x, w[c].y, w[c].z, w[c].w};
         uint32_t v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (e0 + j < numel && (inv + (float)ws[j] * inv) <= p) ? 1u : 0u;
-        if constexpr (BITS) {
-            // 16 consecutive lanes = one 64-element word (t % 16 == 0 at lane 16q; base % 64 == 0)
-            const int sh = 4 * (int)(threadIdx.x & 15);
-            const uint32_t nib = v[0] | (v[1] << 1) | (v[2] << 2) | (v[3] << 3);
-            uint32_t lo32 = sh < 32 ? nib << sh : 0u, hi32 = sh >= 32 ? nib << (sh - 32) : 0u;
-#pragma unroll
-            for (int d = 1; d < 16; d <<= 1) {
-                lo32 |= (uint32_t)__shfl_xor((int)lo32, d, 64);
-                hi32 |= (uint32_t)__shfl_xor((int)hi32, d, 64);
-            }
-            if ((threadIdx.x & 15) == 0 && e0 < numel)
-                reinterpret_cast<uint64_t*>(mask)[(base + e0) >> 6] = ((uint64_t)hi32 << 32) | lo32;
-        } else if (e0 < numel) {
+        for (int j = 0; j < 4; ++j) v[j] = (any && ws[j] <= thr) ? 1u : 0u;
+        if (e0 < numel) {
             uint8_t* m = reinterpret_cast<uint8_t*>(mask) + base + e0;
             if (e0 + 4 <= numel) {
                 *reinterpret_cast<uchar4*>(m) = make_uchar4(v[0], v[1], v[2], v[3]);
@@ -868,6 +876,34 @@ extern "C" GA_API void ga_sparta_gap_table(double p, uint64_t* table) {
     }
 }
 
+// rocrand's uniform of a 32-bit word w is RN(2^-32 + w * 2^-32) (float; the
+// product is exact, so fused or not it rounds once) and is nondecreasing in w,
+// so {w : uniform(w) <= p} is [0, thr]: the largest such w, found by bisection
+// with the same float arithmetic; false when no word qualifies (p < 2^-32 or
+// NaN).  The kernels then compare integers.
+static bool tb_threshold(float p, uint32_t* thr) {
+    const float inv = ldexpf(1.f, -32);
+    auto sel = [&](uint32_t w) {
+        volatile float x = (float)w * inv;
+        volatile float u = x + inv;
+        return u <= p;
+    };
+    *thr = 0u;
+    if (!sel(0u)) return false;
+    uint32_t lo = 0u, hi = 0xFFFFFFFFu;
+    if (sel(hi)) {
+        *thr = hi;
+        return true;
+    }
+    while (hi - lo > 1u) {  // sel(lo) && !sel(hi)
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (sel(mid)) lo = mid;
+        else hi = mid;
+    }
+    *thr = lo;
+    return true;
+}
+
 static Pred make_pred(const void* mask, int mask_format, uint64_t seed, uint64_t iteration, double p,
                       const int64_t* skip, int64_t nskip) {
     Pred P;
@@ -875,7 +911,8 @@ static Pred make_pred(const void* mask, int mask_format, uint64_t seed, uint64_t
     P.bits = mask_format == GA_MASK_BITS ? (const uint64_t*)mask : nullptr;
     P.ttab = nullptr;
     P.tn = 0;
-    P.tp = 0.f;
+    P.tthr = 0u;
+    P.tany = 0;
     P.toff0 = P.tstep = 0;
     P.tseedoff = nullptr;
     P.tkey = make_uint2(0u, 0u);
@@ -883,7 +920,7 @@ static Pred make_pred(const void* mask, int mask_format, uint64_t seed, uint64_t
         const ga_sparta_torch_draw* d = (const ga_sparta_torch_draw*)mask;
         P.ttab = d->table;
         P.tn = d->ntens;
-        P.tp = d->p;
+        P.tany = tb_threshold(d->p, &P.tthr) ? 1 : 0;
         P.toff0 = d->offset0;
         P.tstep = d->offset_step;
         P.tseedoff = d->seedoff;
@@ -997,12 +1034,14 @@ extern "C" GA_API int ga_sparta_torch_bernoulli(const int64_t* table, int32_t nt
     GA_REQUIRE(offset0 % 4 == 0 && offset_step % 4 == 0, "ga_sparta_torch_bernoulli: offsets must be multiples of 4");
     if (ntens == 0 || nblocks == 0) return GA_OK;
     GA_REQUIRE(table && mask && ((uintptr_t)mask % 8) == 0, "ga_sparta_torch_bernoulli: null table/mask or mask alignment");
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kSpBlock), 0, stream, table, (int)ntens, p,
+    uint32_t thr;
+    const int32_t any = tb_threshold(p, &thr) ? 1 : 0;
+    auto go = [&](auto kern, int block) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(block), 0, stream, table, (int)ntens, thr, any,
                            make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)), offset0, offset_step, seedoff, mask);
     };
-    if (mask_format == GA_MASK_BITS) go(sparta_torch_bernoulli_kernel<true>);
-    else go(sparta_torch_bernoulli_kernel<false>);
+    if (mask_format == GA_MASK_BITS) go(sparta_torch_bernoulli_kernel<true>, kTbWordLanes);
+    else go(sparta_torch_bernoulli_kernel<false>, kSpBlock);
     return check_launch("ga_sparta_torch_bernoulli");
 }
 

@@ -933,7 +933,12 @@ def test_sparta_inplace_bernoulli_is_the_reference_draw(mode):
     assert (state.graph is not None) == (mode == "graph")
 
 
-@pytest.mark.parametrize("numel,p", [(1, 0.5), (7, 0.3), (4096 * 3 + 2, 0.005), (2_000_003, 0.005), (100_000, 0.9)])
+# p edges for the kernels' integer threshold (tb_threshold): none / every
+# element, p = 2^-32 (only a zero word qualifies), p below 2^-32, the largest
+# float below 1 (the top words round to a uniform of 1.0 and are not selected)
+@pytest.mark.parametrize("numel,p", [(1, 0.5), (7, 0.3), (4096 * 3 + 2, 0.005), (2_000_003, 0.005), (100_000, 0.9),
+                                     (4096 + 70, 0.0), (4096 + 70, 1.0), (50_000, 2.0 ** -32), (50_000, 1e-10),
+                                     (300_001, 0.99999994)])
 def test_torch_gpu_bernoulli_oracle_and_kernel(numel, p):
     """oracle.sparta.torch_gpu_bernoulli restates ATen's HIP bernoulli kernel
     (pinned here against torch.bernoulli(torch.full(...)) on this GPU), and
