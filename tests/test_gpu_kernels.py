@@ -967,20 +967,21 @@ def test_torch_gpu_bernoulli_oracle_and_kernel(numel, p):
     assert np.array_equal(gb[1:1 + -(-numel // 64)], osparta.pack_mask(want))
 
 
-@pytest.mark.parametrize("layout,K", [("elem", 32), ("rows", 3)])
-def test_sparta_in_kernel_reference_draw(layout, K):
+@pytest.mark.parametrize("layout,K,p", [("elem", 32, 0.05), ("rows", 3, 0.05), ("elem", 32, 0.3), ("elem", 8, 0.9)])
+def test_sparta_in_kernel_reference_draw(layout, K, p):
     """GA_MASK_TORCH: the average kernel draws the reference's masks itself
     (draw_masks(defer=True) -> ops.TorchDraw) -- the same averages as with the
     fused draw's packed mask and the oracle's restatement of torch's stream,
     and the generator advanced identically; a grad-less tensor is skipped and
-    tensor ends fall inside 64-element groups."""
+    tensor ends fall inside 64-element groups; p = 0.3 / 0.9 list several
+    windows per wave tile."""
     from gym_amd import ops
     from gym_amd.arena import ArenaLayout
     from gym_amd.strategy.sparta import MaskDraw, RandomIndexSelector, draw_masks
     shapes = [(300, 77), (768,), (5, 9), (1000, 64), (3,)]
     L = ArenaLayout(shapes)
     params = [torch.zeros(s, device=DEV) for s in shapes]
-    sel = RandomIndexSelector(0.05)
+    sel = RandomIndexSelector(p)
     skip = {2}
     rng = np.random.default_rng(K)
     x = rng.standard_normal((K, L.n)).astype(np.float32)
@@ -1006,7 +1007,7 @@ def test_sparta_in_kernel_reference_draw(layout, K):
     for j, (o, nn) in enumerate(zip(L.offsets, L.numels)):
         if j in skip:
             continue
-        want_mask[o:o + nn] = osparta.torch_gpu_bernoulli(nn, 0.05, seed, off0 + 12 * i)
+        want_mask[o:o + nn] = osparta.torch_gpu_bernoulli(nn, p, seed, off0 + 12 * i)
         i += 1
     want = osparta.sparse_average(list(x), want_mask)
     for k in range(K):
