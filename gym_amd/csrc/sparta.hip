@@ -163,9 +163,13 @@ __device__ __forceinline__ uint64_t torch_bits64(const Pred& P, int64_t e0) {
 
 // Selection bits of the 64 elements starting at element `e0` (e0 % 64 == 0);
 // tab: the gap table in LDS.
+// SRC: 0 = whichever source P names; 1 = the in-kernel reference draw only;
+// 2 = anything but it (per-source instantiations keep each kernel's registers
+// to what its source needs)
+template <int SRC = 0>
 __device__ __forceinline__ uint64_t pred_bits64(const Pred& P, const uint64_t* tab, int64_t e0, int64_t n) {
     uint64_t bits = 0;
-    if (P.ttab) {
+    if (SRC == 1 || (SRC == 0 && P.ttab)) {
         bits = torch_bits64(P, e0);
         return e0 + 64 <= n ? bits : bits & ((1ull << (n - e0)) - 1ull);
     }
@@ -597,13 +601,20 @@ struct WaveBatchDpp {
     }
 };
 
-template <typename T, int KQ>
-__global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(Pred P, int64_t n, T* __restrict__ src,
+// 8 waves per SIMD: the per-source instantiations fit 64 VGPRs without spills
+// (67 / 63 unconstrained); Philox mode 0.048 -> 0.045 ms, reference draw
+// unchanged (profiles/r02z_ab_sparta_split_wpe.txt)
+#ifndef GA_SP_WPE
+#define GA_SP_WPE 8
+#endif
+#define GA_SP_WPE_ATTR __attribute__((amdgpu_waves_per_eu(GA_SP_WPE, GA_SP_WPE)))
+template <typename T, int KQ, int SRC>
+__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_average_wave_kernel(Pred P, int64_t n, T* __restrict__ src,
                                                                                int64_t ld, float divisor) {
     using B = WaveBatchDpp<T, KQ>;
     __shared__ uint64_t tab[kGapTable];
     __shared__ uint16_t lists[GA_SP_WAVES][kWList];
-    load_gap_table(P, tab);
+    if (SRC != 1) load_gap_table(P, tab);  // the reference draw has no gap table
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint16_t* list = lists[wid];
     const int64_t t = (int64_t)blockIdx.x * GA_SP_WAVES + wid;
@@ -615,7 +626,7 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_wave_kernel(P
 #pragma unroll
     for (int g = 0; g < kWGroups; ++g) {
         const int64_t eg = e0 + (int64_t)g * kSpPerThread;
-        bits[g] = eg < n ? pred_bits64(P, tab, eg, n) : 0ull;
+        bits[g] = eg < n ? pred_bits64<SRC>(P, tab, eg, n) : 0ull;
         c += __popcll(bits[g]);
     }
     int x = c;
@@ -654,11 +665,11 @@ static bool launch_average_wave(hipStream_t stream, const Pred& P, int64_t n, vo
     const dim3 grid((unsigned)ceil_div(ceil_div(n, kWTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, (T*)src, ld, divisor); };
     switch (K) {
-        case 4: go(sparta_average_wave_kernel<T, 1>); return true;
-        case 8: go(sparta_average_wave_kernel<T, 2>); return true;
-        case 16: go(sparta_average_wave_kernel<T, 4>); return true;
-        case 32: go(sparta_average_wave_kernel<T, 8>); return true;
-        case 64: go(sparta_average_wave_kernel<T, 16>); return true;
+        case 4: P.ttab ? go(sparta_average_wave_kernel<T, 1, 1>) : go(sparta_average_wave_kernel<T, 1, 2>); return true;
+        case 8: P.ttab ? go(sparta_average_wave_kernel<T, 2, 1>) : go(sparta_average_wave_kernel<T, 2, 2>); return true;
+        case 16: P.ttab ? go(sparta_average_wave_kernel<T, 4, 1>) : go(sparta_average_wave_kernel<T, 4, 2>); return true;
+        case 32: P.ttab ? go(sparta_average_wave_kernel<T, 8, 1>) : go(sparta_average_wave_kernel<T, 8, 2>); return true;
+        case 64: P.ttab ? go(sparta_average_wave_kernel<T, 16, 1>) : go(sparta_average_wave_kernel<T, 16, 2>); return true;
         default: return false;
     }
 }
