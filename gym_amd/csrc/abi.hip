@@ -38,12 +38,12 @@ __global__ __launch_bounds__(256) void stream_copy_kernel(const float4* __restri
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int64_t i = base + u * 256;
-        if (i < nvec) v[u] = src[i];
+        if (i < nvec) v[u] = stream_load(src + i);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int64_t i = base + u * 256;
-        if (i < nvec) dst[i] = v[u];
+        if (i < nvec) stream_store(dst + i, v[u]);
     }
 }
 

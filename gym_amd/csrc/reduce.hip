@@ -48,7 +48,7 @@ __global__ __launch_bounds__(kBlock) void replica_mean_kernel(
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
             for (int64_t k = 0; k < K; ++k) {
-                const V raw = reinterpret_cast<const V*>(replica_ptr(src, rows, k, ld_src))[v];
+                const V raw = stream_load(reinterpret_cast<const V*>(replica_ptr(src, rows, k, ld_src)) + v);
                 float f[4];
                 Vec4<T>::unpack(raw, f);
 #pragma unroll
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kBlock) void replica_mean_kernel(
                 for (int e = 0; e < 4; ++e) acc[e] = acc[e] / divisor;
             }
             const V out = Vec4<T>::pack(acc);
-            for (int64_t j = 0; j < K_out; ++j) reinterpret_cast<V*>(dst + j * ld_dst)[v] = out;
+            for (int64_t j = 0; j < K_out; ++j) stream_store(reinterpret_cast<V*>(dst + j * ld_dst) + v, out);
         }
     } else {
         chunk_range(n, lo, hi);
@@ -109,20 +109,20 @@ __global__ __launch_bounds__(kBlock) void diloco_outer_kernel(
 #pragma unroll 8
             for (int64_t k = 0; k < K; ++k) {
                 float f[4];
-                Vec4<T>::unpack(reinterpret_cast<const V*>(src + k * ld_src)[v], f);
+                Vec4<T>::unpack(stream_load(reinterpret_cast<const V*>(src + k * ld_src) + v), f);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) acc[e] += f[e];
             }
             float m[4], b[4] = {0.f, 0.f, 0.f, 0.f};
-            Vec4<M>::unpack(reinterpret_cast<const VM*>(master)[v], m);
-            if (has_mom && !op.first_step) Vec4<M>::unpack(reinterpret_cast<const VM*>(mom)[v], b);
+            Vec4<M>::unpack(stream_load(reinterpret_cast<const VM*>(master) + v), m);
+            if (has_mom && !op.first_step) Vec4<M>::unpack(stream_load(reinterpret_cast<const VM*>(mom) + v), b);
             float out[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) out[e] = outer_update(acc[e], m[e], b[e], op);
-            reinterpret_cast<VM*>(master)[v] = Vec4<M>::pack(m);
-            if (has_mom) reinterpret_cast<VM*>(mom)[v] = Vec4<M>::pack(b);
+            stream_store(reinterpret_cast<VM*>(master) + v, Vec4<M>::pack(m));
+            if (has_mom) stream_store(reinterpret_cast<VM*>(mom) + v, Vec4<M>::pack(b));
             const V o = Vec4<T>::pack(out);
-            for (int64_t j = 0; j < K_out; ++j) reinterpret_cast<V*>(dst + j * ld_dst)[v] = o;
+            for (int64_t j = 0; j < K_out; ++j) stream_store(reinterpret_cast<V*>(dst + j * ld_dst) + v, o);
         }
     } else {
         chunk_range(n, lo, hi);
