@@ -54,21 +54,21 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ par
     const int64_t lo = (int64_t)blockIdx.x * kOptChunk;
     const int64_t hi = lo + kOptChunk < nv ? lo + kOptChunk : nv;
     for (int64_t i = lo + threadIdx.x; i < hi; i += kOptBlock) {
-        float4 p = reinterpret_cast<float4*>(param)[i];
-        float4 g = reinterpret_cast<const float4*>(grad)[i];
-        float4 m = reinterpret_cast<float4*>(m_)[i];
-        float4 v = reinterpret_cast<float4*>(v_)[i];
+        float4 p = stream_load(reinterpret_cast<const float4*>(param) + i);
+        float4 g = stream_load(reinterpret_cast<const float4*>(grad) + i);
+        float4 m = stream_load(reinterpret_cast<const float4*>(m_) + i);
+        float4 v = stream_load(reinterpret_cast<const float4*>(v_) + i);
         if (scale) {
             g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
-            reinterpret_cast<float4*>(grad)[i] = g;  // clip_grad_norm_ leaves the clipped grads
+            stream_store(reinterpret_cast<float4*>(grad) + i, g);  // clip_grad_norm_ leaves the clipped grads
         }
         float gg[4] = {g.x, g.y, g.z, g.w};
         float pp[4] = {p.x, p.y, p.z, p.w}, mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], ap);
-        reinterpret_cast<float4*>(param)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-        reinterpret_cast<float4*>(m_)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-        reinterpret_cast<float4*>(v_)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        stream_store(reinterpret_cast<float4*>(param) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
+        stream_store(reinterpret_cast<float4*>(m_) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
+        stream_store(reinterpret_cast<float4*>(v_) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
     }
     // scalar tail (n % 4), handled by the last workgroup
     if (blockIdx.x == gridDim.x - 1) {
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const T* __restrict__ 
     using V = typename Vec4<T>::type;
     for (int64_t i = (int64_t)blockIdx.x * kOptBlock + threadIdx.x; i < nv; i += stride) {
         float f[4];
-        Vec4<T>::unpack(reinterpret_cast<const V*>(x)[i], f);
+        Vec4<T>::unpack(stream_load(reinterpret_cast<const V*>(x) + i), f);
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc = fmaf(f[e], f[e], acc);
     }
