@@ -567,7 +567,8 @@ __device__ __forceinline__ void wave_sync() {
 // the lanes with DPP row shifts (lane q adds its four values to lane q - 1's
 // running sum: the oracle's sequential order exactly), then the last lane's
 // average is broadcast back.  No LDS staging, no wave_sync; NP passes (8
-// elements each at K = 32) in flight.  An LDS-staged form (values written at an
+// elements each at K = 32) in flight; the lines are loaded and stored
+// non-temporally (0.045 -> 0.041 ms, profiles/r02z_ab_sparta_nt.txt).  An LDS-staged form (values written at an
 // odd stride, summed by one lane per element) measured 5% slower
 // (profiles/r02x_ab_sparta_batch.txt).
 #ifndef GA_SP_DPP_PASSES
@@ -587,7 +588,7 @@ struct WaveBatchDpp {
 #pragma unroll
         for (int u = 0; u < NP; ++u) {
             const int e = u * EPP + el;
-            if (e < ne) v[u] = *reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q);
+            if (e < ne) v[u] = stream_load(reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q));
         }
 #pragma unroll
         for (int u = 0; u < NP; ++u) {
@@ -606,7 +607,7 @@ struct WaveBatchDpp {
             const float avg = __shfl(a / divisor, (lane & ~(KQ - 1)) | (KQ - 1), 64);
             if (e < ne) {
                 const float w[4] = {avg, avg, avg, avg};
-                *reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q) = Vec4<T>::pack(w);
+                stream_store(reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q), Vec4<T>::pack(w));
             }
         }
     }
