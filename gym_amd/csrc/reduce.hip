@@ -5,7 +5,9 @@
 // 8 B for bf16); workgroup b owns the contiguous vectors [b*kChunk,
 // (b+1)*kChunk) (measured on MI355X: 5.1 TB/s for the K=8 DiLoCo stream vs
 // 4.7 TB/s with a grid-stride loop; a plain float4 copy peaks at 5.2-5.5 TB/s
-// on the same box, tools/ubench_stream.hip).  Each lane issues the K replica loads
+// on the same box, tools/ubench_stream.hip); every stream is loaded and stored
+// non-temporally (stream_load / stream_store: 1.93 -> 1.88 ms for the K = 8 step
+// on one box, profiles/r02z_ab_stream_nt.txt).  Each lane issues the K replica loads
 // of one vector back to back (the k loop is unrolled so the loads are in
 // flight together) and sums them in ascending k, so the result does not
 // depend on the launch geometry.  dst may alias src (in-place average): each
