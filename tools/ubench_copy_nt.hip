@@ -36,6 +36,23 @@ __global__ __launch_bounds__(256) void copy4(const f4* __restrict__ src, f4* __r
     }
 }
 
+// U float4 per lane, B threads per workgroup, both hints (shape sweep)
+template <int U, int B>
+__global__ __launch_bounds__(B) void copy_u(const f4* __restrict__ src, f4* __restrict__ dst, long nvec) {
+    const long base = (long)blockIdx.x * (U * B) + threadIdx.x;
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const long i = base + (long)u * B;
+        if (i < nvec) v[u] = __builtin_nontemporal_load(src + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const long i = base + (long)u * B;
+        if (i < nvec) __builtin_nontemporal_store(v[u], dst + i);
+    }
+}
+
 // grid-stride form with a fixed grid (8 workgroups per CU)
 template <bool NTS>
 __global__ __launch_bounds__(256) void copy_gs(const f4* __restrict__ src, f4* __restrict__ dst, long nvec) {
@@ -56,7 +73,7 @@ int main() {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (long bytes : {1L << 30, 2L << 30, maxb}) {
+    for (long bytes : {1L << 30, maxb}) {
         const long nvec = bytes / 16;
         const unsigned g = (unsigned)((nvec + 1023) / 1024);
         auto run = [&](const char* name, auto launch) {
@@ -80,6 +97,12 @@ int main() {
         run("grid-stride 2048 wg", [&] { copy_gs<false><<<2048, 256>>>(a, b, nvec); });
         run("grid-stride 2048 nt store", [&] { copy_gs<true><<<2048, 256>>>(a, b, nvec); });
         run("plain (again)", [&] { copy4<false, false><<<g, 256>>>(a, b, nvec); });
+        run("nt U=2 B=256", [&] { copy_u<2, 256><<<(unsigned)((nvec + 511) / 512), 256>>>(a, b, nvec); });
+        run("nt U=8 B=256", [&] { copy_u<8, 256><<<(unsigned)((nvec + 2047) / 2048), 256>>>(a, b, nvec); });
+        run("nt U=4 B=512", [&] { copy_u<4, 512><<<(unsigned)((nvec + 2047) / 2048), 512>>>(a, b, nvec); });
+        run("nt U=4 B=1024", [&] { copy_u<4, 1024><<<(unsigned)((nvec + 4095) / 4096), 1024>>>(a, b, nvec); });
+        run("nt U=16 B=256", [&] { copy_u<16, 256><<<(unsigned)((nvec + 4095) / 4096), 256>>>(a, b, nvec); });
+        run("nt U=4 B=256 (again)", [&] { copy_u<4, 256><<<g, 256>>>(a, b, nvec); });
     }
     return 0;
 }
