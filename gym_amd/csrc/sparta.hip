@@ -581,6 +581,35 @@ struct WaveBatchDpp {
     __device__ __forceinline__ static float shr1(float a) {  // lane i <- lane i - 1 within each 16-lane row
         return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x111, 0xf, 0xf, true));
     }
+    // select form: the ascending-replica sum of each listed element goes to
+    // vals[pos0 + e] (pos < cap), nothing is written back
+    __device__ __forceinline__ static void sums(const T* src, int64_t ld, int64_t tile0, const uint16_t* list,
+                                                int b0, int ne, int lane, T* vals, int64_t pos0, int64_t cap) {
+        const int q = lane % KQ, el = lane / KQ;
+        V v[NP];
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int e = u * EPP + el;
+            if (e < ne) v[u] = stream_load(reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q));
+        }
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            if (u * EPP >= ne) break;  // wave-uniform
+            const int e = u * EPP + el;
+            float f[4] = {0.f, 0.f, 0.f, 0.f};
+            if (e < ne) Vec4<T>::unpack(v[u], f);
+            float a = 0.f;
+#pragma unroll
+            for (int s = 0; s < KQ; ++s) {
+                float left = KQ > 1 ? shr1(a) : 0.f;
+                if (q == 0) left = 0.f;
+                const float c = (((left + f[0]) + f[1]) + f[2]) + f[3];
+                a = q == s ? c : a;
+            }
+            const int64_t pos = pos0 + b0 + e;
+            if (q == KQ - 1 && e < ne && pos < cap) Elem<T>::store(vals + pos, a);
+        }
+    }
     __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0,
                                                int ne, int lane, float divisor) {
         const int q = lane % KQ, el = lane / KQ;
@@ -668,6 +697,86 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_averag
         const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
         for (int b0 = 0; b0 < wtot; b0 += B::EB)
             B::run(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, divisor);
+    }
+}
+
+// The exchange path's select on the [n, K] layout in the wave form: a
+// workgroup of GA_SP_WAVES wave tiles is exactly one count/scan tile (kSpTile),
+// so its packed-list base comes from tile_offsets and each wave adds the
+// totals of the waves before it.  Every selected element's index goes to idx,
+// its K-replica sum (ascending replica order, the DPP lane walk) to vals.
+static_assert(GA_SP_WAVES * kWTile == kSpTile, "select wave kernel: a workgroup is one count/scan tile");
+template <typename T, int KQ, int SRC>
+__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select_wave_kernel(
+    Pred P, int64_t n, const int32_t* __restrict__ tile_offsets, const T* __restrict__ src, int64_t ld, int64_t cap,
+    int32_t* __restrict__ idx, T* __restrict__ vals) {
+    using B = WaveBatchDpp<T, KQ>;
+    __shared__ uint64_t tab[kGapTable];
+    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
+    __shared__ int wave_tot[GA_SP_WAVES];
+    if (SRC != 1) load_gap_table(P, tab);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint16_t* list = lists[wid];
+    const int64_t tile0 = ((int64_t)blockIdx.x * GA_SP_WAVES + wid) * kWTile;
+    const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
+    const uint64_t bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
+    const int c = __popcll(bits);
+    int x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    const int total = __shfl(x, 63, 64);
+    const int local0 = x - c;
+    if (lane == 0) wave_tot[wid] = total;
+    __syncthreads();
+    int64_t pos0 = tile_offsets[blockIdx.x];
+    for (int w = 0; w < wid; ++w) pos0 += wave_tot[w];
+    {
+        int l = local0;
+        uint64_t b = bits;
+        while (b) {
+            const int j = __builtin_ctzll(b);
+            b &= b - 1;
+            const int64_t pos = pos0 + l;
+            if (idx && pos < cap) idx[pos] = (int32_t)(e0 + j);
+            ++l;
+        }
+    }
+    if (!vals) return;
+    for (int w0 = 0; w0 < total; w0 += kWList) {  // one window unless p is large
+        {
+            int l = local0;
+            uint64_t b = bits;
+            while (b) {
+                const int j = __builtin_ctzll(b);
+                b &= b - 1;
+                if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * kSpPerThread + j);
+                ++l;
+            }
+        }
+        wave_sync();
+        const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
+        for (int b0 = 0; b0 < wtot; b0 += B::EB)
+            B::sums(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, vals, pos0 + w0, cap);
+    }
+}
+
+template <typename T>
+static bool launch_select_wave(hipStream_t stream, const Pred& P, int64_t n, const int32_t* tile_offsets,
+                               const void* src, int64_t ld, int64_t K, int64_t cap, int32_t* idx, void* vals) {
+    const dim3 grid((unsigned)ceil_div(n, (int64_t)kSpTile)), block(64 * GA_SP_WAVES);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, tile_offsets, (const T*)src, ld, cap, idx, (T*)vals);
+    };
+    switch (K) {
+        case 4: P.ttab ? go(sparta_select_wave_kernel<T, 1, 1>) : go(sparta_select_wave_kernel<T, 1, 2>); return true;
+        case 8: P.ttab ? go(sparta_select_wave_kernel<T, 2, 1>) : go(sparta_select_wave_kernel<T, 2, 2>); return true;
+        case 16: P.ttab ? go(sparta_select_wave_kernel<T, 4, 1>) : go(sparta_select_wave_kernel<T, 4, 2>); return true;
+        case 32: P.ttab ? go(sparta_select_wave_kernel<T, 8, 1>) : go(sparta_select_wave_kernel<T, 8, 2>); return true;
+        case 64: P.ttab ? go(sparta_select_wave_kernel<T, 16, 1>) : go(sparta_select_wave_kernel<T, 16, 2>); return true;
+        default: return false;
     }
 }
 
@@ -870,6 +979,11 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
     if (v4 && !tile_offsets && !vals && divisor > 0.f && launch_average_wave<T>(stream, P, n, (void*)src, R.ei, K,
                                                                                 divisor))
         return check_launch("ga_sparta_average_local(wave)");
+#ifndef GA_SP_NO_WAVE_SELECT
+    if (v4 && tile_offsets && divisor == 0.f &&
+        launch_select_wave<T>(stream, P, n, tile_offsets, src, R.ei, K, cap, idx, vals))
+        return check_launch("ga_sparta_select(wave)");
+#endif
     if (v4)
         hipLaunchKernelGGL((sparta_select_kernel<T, true>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
                            tile_offsets, (T*)src, K, R, cap, idx, (T*)vals, divisor);
