@@ -268,7 +268,14 @@ def bench_diloco(args, coll, dev):
     eng(reps)  # first outer step (momentum buffer created); timed steps use the warm buffer
     timer.on = True
     t = timed_loop(lambda: eng(reps), args.steps, args.warmup, coll)
-    kern_ms = timer.mean_ms()
+    kern_single = timer.mean_ms()
+    timer.on = False
+    kern_ms, kern_how = kern_single, "HIP events around each launch"
+    if coll.world == 1 and not args.pmc_child:
+        # one launch per step: time it queued back to back (what rocprofv3's kernel
+        # durations measure; single-launch events add the host's launch gap)
+        kern_ms = queued_ms(lambda: eng(reps), max(args.steps, 10), dev)
+        kern_how = "HIP events around back-to-back launches queued behind streaming copies (queued_ms)"
     K_total = K * coll.world
     n_params = numel(shapes)
     value = K_total * 4 * n_params / t / 1e9
@@ -291,6 +298,8 @@ def bench_diloco(args, coll, dev):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_over_alg": round(traffic / alg_bytes, 6) if traffic else None, "traffic_source": tnote,
             "kernel": "ga_diloco_outer", "bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),
+            "kernel_timing": kern_how,
+            "kernel_ms_single_launch_events": round(kern_single, 4) if kern_single is not None else None,
             "copy_GBps": round(copy, 1) if copy else None,
             "frac_of_copy": round(achieved / copy, 4) if copy else None},
     }
@@ -548,6 +557,7 @@ def bench_inner_adamw(args, coll, dev, model="gpt2-124m", max_norm=1.0):
 
 
 def main():
+    t_start = time.perf_counter()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -570,11 +580,16 @@ def main():
     # host-side legs first, while this process has not touched the GPU (the
     # children are started by fork+exec; none of them runs in a GPU-initialised process)
     cpu = None
+    legs = {}
+    t0 = time.perf_counter()
     if single and not args.no_cpu_baseline and args.only is None:
         cpu = cpu_baseline_diloco(args.model, args.replicas)
+    legs["cpu_baseline_s"] = round(time.perf_counter() - t0, 1)
     args.pmc = (None, "not measured (N > 1 or --no-pmc)")
+    t0 = time.perf_counter()
     if single and not args.no_pmc and args.only is None and not under_profiler():
         args.pmc = pmc_traffic_live(args)
+    legs["pmc_passes_s"] = round(time.perf_counter() - t0, 1)
 
     coll = setup_dist(args.gpus)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -608,10 +623,12 @@ def main():
             runs.insert(0, ("diloco_1_node_per_gpu", diloco_1))
         for name, fn in runs:
             torch.cuda.empty_cache()
+            t_leg = time.perf_counter()
             try:
                 extras[name] = fn(args, coll, dev)
             except Exception as e:  # keep the headline line even if an extra fails
                 extras[name] = {"error": repr(e)[:300]}
+            extras[name]["leg_s"] = round(time.perf_counter() - t_leg, 1)
     if coll.rank != 0:
         if coll.world > 1:
             dist.barrier()
@@ -646,6 +663,8 @@ def main():
         line["rehearsal"] = "world-1 RCCL group with forced exchange: the multi-GPU code paths, not a measurement"
     if extras:
         line["extras"] = extras
+    line["bench_wall_s"] = round(time.perf_counter() - t_start, 1)  # this process, CPU baseline + PMC passes included
+    line["host_legs_s"] = legs
     print(json.dumps(line), flush=True)
     if coll.world > 1:
         dist.barrier()

@@ -416,8 +416,9 @@ class PipelinedDeMoCodec:
     order are the ones of the unpipelined codec, so results are identical.
     Same call signature as DeMoCodec.__call__ (no custom all_gather)."""
 
-    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32, pieces=4):
+    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32, pieces=None):
         self.coll = coll
+        pieces = DEMO_PIECES if pieces is None else pieces
         groups = split_tensors(layout.numels, max(1, int(pieces)))
         self.codecs = [DeMoCodec(coll, K_local, layout.subset(g), device, chunk=chunk, topk=topk) for g in groups]
         # every piece runs the kernel family the whole plan would (the wave-per-chunk

@@ -19,7 +19,17 @@ arenas within it ((s-1)·N received per rank instead of the reference's
 the gathered rows averages them.  With a caller-supplied process group the
 island step falls back to one all-gather over that group + the same mean over
 the member rows.
+
+Sub-communicators are bounded: each costs a store barrier over the world to
+create and, under RCCL, a communicator with its own GPU buffers, and rank 0
+reshuffles every round, so up to C(K, s) member sets appear.  They are used
+only while every island of a round is cached or fits under
+MAX_ISLAND_GROUPS (and never when C(K, s) alone exceeds it, e.g. 1820 sets at
+K = 16, s = 4); otherwise the round takes the world all-gather + member-row
+mean.  The choice depends only on the broadcast permutation and the cache, so
+every rank makes the same one.
 """
+import math
 import random
 from typing import Optional, Set, Union
 
@@ -31,6 +41,9 @@ from ..comm import Collective
 from ..engine import MeanReduce
 from .communicate_optimize_strategy import CommunicateOptimizeStrategy, CommunicationModule
 from .optim import OptimSpec
+
+# cached island sub-communicators per process (bounded, no per-round growth)
+MAX_ISLAND_GROUPS = 32
 
 
 class AveragingCommunicator(CommunicationModule):
@@ -54,19 +67,34 @@ class AveragingCommunicator(CommunicationModule):
                 return island
         return None
 
-    def _island_collective(self, members: Set[int]):
-        """Collective over `members` (a sub-communicator).  Every island of this
-        communication that is new gets its group here, on every rank, in the
-        permutation order rank 0 broadcast: dist.new_group is collective over
-        the world, so all ranks create the same groups in the same order."""
+    def _groups_possible(self, num_nodes: int) -> int:
+        """Distinct multi-member island sets rank 0's shuffles can produce."""
+        s = self.island_size if self.island_size is not None else num_nodes
+        n = math.comb(num_nodes, s) if s > 1 else 0
+        r = num_nodes % s
+        return n + (math.comb(num_nodes, r) if r > 1 else 0)
+
+    def _island_collective(self, members: Set[int], num_nodes: int):
+        """(True, Collective over `members` or None for an island of one) when
+        this round's islands use sub-communicators; (False, None) for the
+        world all-gather path, which every rank then joins (islands of one
+        included).  Every island of this communication that is new gets its
+        group here, on every rank, in the permutation order rank 0 broadcast:
+        dist.new_group is collective over the world, so all ranks create the
+        same groups in the same order.  The group cache never exceeds
+        MAX_ISLAND_GROUPS (module docstring)."""
+        if self._groups_possible(num_nodes) > MAX_ISLAND_GROUPS:
+            return False, None
+        keys = [tuple(sorted(i)) for i in self._islands]
+        new = [k for k in dict.fromkeys(keys) if len(k) > 1 and k not in self._groups]
+        if len(self._groups) + len(new) > MAX_ISLAND_GROUPS:
+            return False, None
         me = dist.get_rank()
-        for island in self._islands:
-            key = tuple(sorted(island))
-            if len(key) > 1 and key not in self._groups:
-                g = dist.new_group(list(key))
-                self._groups[key] = (g, Collective(g) if me in island else None)
+        for key in new:
+            g = dist.new_group(list(key))
+            self._groups[key] = (g, Collective(g) if me in key else None)
         key = tuple(sorted(members))
-        return self._groups[key][1] if len(key) > 1 else None
+        return True, (self._groups[key][1] if len(key) > 1 else None)
 
     def _average_models(self, model, island_members: Set[int], num_nodes: int) -> None:
         s = self.strategy
@@ -78,14 +106,15 @@ class AveragingCommunicator(CommunicationModule):
             self._mean(a.flat.view(1, -1))
             return
         members = sorted(island_members)
-        coll = self._island_collective(island_members) if s.coll.group is None and self._islands else None
-        if len(members) == 1:  # (0 + x) / 1, as the reference's sum([x]) / 1
+        sub, coll = (self._island_collective(island_members, num_nodes)
+                     if s.coll.group is None and self._islands else (False, None))
+        if sub and len(members) == 1:  # (0 + x) / 1, as the reference's sum([x]) / 1
             ops.replica_mean(a.flat.view(1, -1), a.flat, n=a.n)
             return
-        if coll is not None:
+        if sub:
             rows_all = len(members)
             rows = None  # every gathered row is a member, in ascending rank order
-        else:
+        else:  # every rank joins the world all-gather, islands of one too
             coll, rows_all = s.coll, s.coll.world
             rows = torch.tensor(members, dtype=torch.int32, device=a.device)
         if self._gathered is None or self._gathered.shape[0] < rows_all:

@@ -33,9 +33,11 @@ The ShuffledSequential / Partitioned selectors are the reference's algorithms
 (the same torch draws on the device) feeding the mask-mode kernels.
 """
 import math
+import warnings
 from typing import Optional, Union
 
 import torch
+import torch.distributed as dist
 
 from .. import ops
 from ..engine import Sparta
@@ -78,6 +80,7 @@ class MaskDraw:
         self.graph = None
         self.calls = 0
         self.table = None
+        self.mode = None  # "fused" | "torch": which draw ran last (recorded in __config__ and the bench line)
 
 
 def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=None, defer=False):
@@ -110,6 +113,7 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
     selectors: their get_indices, copied in (eager)."""
     fast = type(selector) is RandomIndexSelector
     if not fast:
+        state.mode = "torch"
         for i, (p, v) in enumerate(zip(params, views)):
             if i in skip:
                 v.zero_()
@@ -129,18 +133,20 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
             else:
                 v.bernoulli_(state.pfull[i])
 
-    on_gpu = bool(params) and params[0].device.type == "cuda"
+    on_gpu = _on_gpu(params)
     # inside a user's graph capture the generator offsets are graph-relative: torch's own kernels then
-    if (on_gpu and MaskDraw.fused and not torch.cuda.is_current_stream_capturing()
-            and fused_draw_matches_torch(params[0].device)):
+    if (on_gpu and MaskDraw.fused and not _capturing()
+            and fused_draw_matches_torch(params[0].device, coll)):
         out = _draw_fused(selector, params, views, skip, state, bits, coll, defer)
         state.calls += 1
+        state.mode = "fused"
         return out
+    state.mode = "torch"
     for i, p in enumerate(params):
         if i not in skip and state.pfull[i] is None:
             state.pfull[i] = torch.full(p.shape, selector.p, device=p.device)
     if (on_gpu and MaskDraw.use_graphs and state.graph is None and state.calls >= 1
-            and not torch.cuda.is_current_stream_capturing()):
+            and not _capturing()):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             body()
@@ -152,39 +158,72 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
     state.calls += 1
 
 
-_FUSED_OK = {}
+def _on_gpu(params):
+    return bool(params) and params[0].device.type == "cuda"
 
 
-def fused_draw_matches_torch(device):
+def _capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+_FUSED_OK = {}      # device -> this process's probe result
+_FUSED_AGREED = {}  # (device, process group) -> the result every rank of the group uses
+_FUSED_WARNED = set()
+
+
+def _probe_fused(device):
     """One-time check per device that ga_sparta_torch_bernoulli still restates
     this torch build's bernoulli kernel: a 3-tensor probe drawn both ways from
     the same generator state (bits, and the state torch leaves behind), the
-    caller's generator state restored afterwards.  False -> draw_masks uses
-    torch's own kernels."""
+    caller's generator state restored afterwards."""
+    dev = torch.device(device)
+    gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+    state = torch.cuda.get_rng_state(dev)
+    try:
+        shapes = [(4099,), (64, 65), (1,)]
+        p = 0.3
+        want = [torch.bernoulli(torch.full(s, p, device=dev)).bool().reshape(-1) for s in shapes]
+        after = torch.cuda.get_rng_state(dev)
+        torch.cuda.set_rng_state(state, dev)
+        numels = [w.numel() for w in want]
+        offs = [sum(-(-m // 64) * 64 for m in numels[:i]) for i in range(len(numels))]
+        table, nb = ops.sparta_bernoulli_table(offs, numels, dev)
+        mask = torch.zeros(offs[-1] + numels[-1], dtype=torch.uint8, device=dev)
+        off0 = gen.get_offset()
+        ops.sparta_torch_bernoulli(table, nb, p, gen.initial_seed(), off0, MaskDraw.offset_step, mask)
+        same_bits = all(torch.equal(mask[a:a + m].bool(), w) for a, m, w in zip(offs, numels, want))
+        gen.set_offset(off0 + MaskDraw.offset_step * len(shapes))
+        same_state = torch.equal(torch.cuda.get_rng_state(dev), after)
+        return bool(same_bits and same_state)
+    finally:
+        torch.cuda.set_rng_state(state, dev)
+
+
+def fused_draw_matches_torch(device, coll=None):
+    """Whether draw_masks may use the fused kernel (_probe_fused, once per
+    device).  With an exchange every rank must take the same path (the fused
+    one broadcasts 16 bytes of generator state, the torch one the packed
+    masks), so the probe results are combined once per group with a MIN
+    all-reduce.  False -> torch's own kernels (same bits, ~10x slower), with
+    a one-time warning; the draw that ran is recorded as MaskDraw.mode."""
     key = str(device)
     if key not in _FUSED_OK:
-        dev = torch.device(device)
-        gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
-        state = torch.cuda.get_rng_state(dev)
-        try:
-            shapes = [(4099,), (64, 65), (1,)]
-            p = 0.3
-            want = [torch.bernoulli(torch.full(s, p, device=dev)).bool().reshape(-1) for s in shapes]
-            after = torch.cuda.get_rng_state(dev)
-            torch.cuda.set_rng_state(state, dev)
-            numels = [w.numel() for w in want]
-            offs = [sum(-(-m // 64) * 64 for m in numels[:i]) for i in range(len(numels))]
-            table, nb = ops.sparta_bernoulli_table(offs, numels, dev)
-            mask = torch.zeros(offs[-1] + numels[-1], dtype=torch.uint8, device=dev)
-            off0 = gen.get_offset()
-            ops.sparta_torch_bernoulli(table, nb, p, gen.initial_seed(), off0, MaskDraw.offset_step, mask)
-            same_bits = all(torch.equal(mask[a:a + m].bool(), w) for a, m, w in zip(offs, numels, want))
-            gen.set_offset(off0 + MaskDraw.offset_step * len(shapes))
-            same_state = torch.equal(torch.cuda.get_rng_state(dev), after)
-            _FUSED_OK[key] = bool(same_bits and same_state)
-        finally:
-            torch.cuda.set_rng_state(state, dev)
-    return _FUSED_OK[key]
+        _FUSED_OK[key] = bool(_probe_fused(device))
+    ok = _FUSED_OK[key]
+    if coll is not None and coll.exchange:
+        gk = (key, id(coll.group))
+        if gk not in _FUSED_AGREED:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=coll.group)
+            _FUSED_AGREED[gk] = bool(int(t.item()))
+        ok = _FUSED_AGREED[gk]
+    if not ok and key not in _FUSED_WARNED:
+        _FUSED_WARNED.add(key)
+        warnings.warn(f"SPARTA: the fused reference draw (ga_sparta_torch_bernoulli) does not match this torch "
+                      f"build's bernoulli kernel on {key} (or on another rank); drawing with torch's per-tensor "
+                      f"kernels instead (same masks, ~0.75 ms instead of ~0.07 ms per step at 124M)",
+                      RuntimeWarning, stacklevel=2)
+    return ok
 
 
 def _i64(v):
@@ -307,6 +346,7 @@ class SparseCommunicator(CommunicationModule):
         self._skip_key = None
         self._skip = None
         self._draw = MaskDraw()
+        self.mask_draw = None  # "philox" | "fused" | "torch" once a step has drawn (read by __config__)
 
     def _init_node(self, model, rank, num_nodes):
         pass
@@ -383,9 +423,12 @@ class SparseCommunicator(CommunicationModule):
                 reps = s.arena.flat.view(1, -1)
                 if self._philox_mode():
                     self._engine(reps, seed=self._shared_seed(), iteration=self.iteration, skip=self._skip_table())
+                    self.mask_draw = "philox"
                 else:
                     m = self._build_mask(model)
                     self._engine(reps, mask=m, mask_cap=self._mask_cap(), mask_shared=self._shared)
+                    self.mask_draw = self._draw.mode
+                s.mask_draw = self.mask_draw
         self.iteration += 1
 
 
@@ -396,3 +439,4 @@ class SPARTAStrategy(CommunicateOptimizeStrategy):
         sparse_comm = SparseCommunicator(index_selector)
         super().__init__(inner_optim=inner_optim, communication_modules=[sparse_comm], **kwargs)
         self.index_selector = index_selector
+        self.mask_draw = None  # which mask draw the last step ran ("philox" | "fused" | "torch")

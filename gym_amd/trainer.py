@@ -150,6 +150,8 @@ class Trainer:
         from .replica import replica_layout
         devs = devices if devices is not None else list(range(max(1, torch.cuda.device_count())))
         layout = replica_layout(num_nodes, devs, self.kwargs.pop("replicas_per_process", "auto"), strategy)
+        # every node's final CPU state dict, kept on the trainer only when asked (K x model size of host memory)
+        keep_node_states = bool(self.kwargs.pop("keep_node_states", False))
         config.kwargs = self.kwargs
         manager = mp.Manager()
         queue = manager.Queue()
@@ -162,7 +164,7 @@ class Trainer:
         for _ in range(num_nodes):
             r, sd = queue.get()
             states[r] = sd
-        self.node_states = [states[r] for r in sorted(states)]  # every node's final state (CPU), node order
+        self.node_states = [states[r] for r in sorted(states)] if keep_node_states else None
         avg = _average_model_states(states)
         if avg is None:
             return None

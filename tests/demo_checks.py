@@ -32,6 +32,32 @@ def firm(g_hat, margins, shape, chunk=64, rel=1e-5, margin_rel=1e-5):
     return out
 
 
+def chunk_max_abs(x, shape, chunk=64):
+    """Per element: max |x| over the element's DeMo chunk (the chunk's scale)."""
+    R, C, n1, n2 = odemo.tensor_view(shape, chunk)
+    a = np.abs(np.asarray(x, np.float64)).reshape(R // n1, n1, C // n2, n2)
+    m = a.max(axis=(1, 3))
+    return np.repeat(np.repeat(m, n1, axis=0), n2, axis=1).reshape(shape)
+
+
+def residual_close(got_d, ref_d, x, margin, shape, chunk=64, rel=1e-6, loose=2e-5, what=""):
+    """The residual delta (demo.py:174-180) where the node's top-k set is firm
+    (k-th margin > 1e-5 of its largest coefficient): within rel x the chunk's
+    scale (max |x| of the encoded input x = decay*delta + lr*grad).  In chunks
+    decided by a near-tie the two implementations may keep different
+    coefficients: there only the tensor-scale bar `loose` applies."""
+    m, scale = margin
+    firm_el = chunk_mask_to_elements(np.asarray(m) > 1e-5 * scale, shape, chunk)
+    err = np.abs(np.asarray(got_d, np.float64) - np.asarray(ref_d, np.float64))
+    lim = rel * chunk_max_abs(x, shape, chunk)
+    bad = np.flatnonzero((err > lim) & firm_el)
+    assert bad.size == 0, (f"{what}: residual delta off by > {rel} x chunk scale at {bad.size} firm elements, "
+                           f"worst {float((err / np.maximum(lim / rel, 1e-30))[firm_el].max()):.3g}")
+    if (~firm_el).any():
+        assert err[~firm_el].max() <= loose * np.abs(np.asarray(x)).max(), what
+    return float(firm_el.mean())
+
+
 def node_margins(deltas, grads, shape, lr, decay, topk=32, chunk=64):
     """(per-chunk k-th margin, coefficient scale) of each node's encoded delta."""
     out = []

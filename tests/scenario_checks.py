@@ -91,6 +91,10 @@ def _torch_masks(kind, device, steps):
 def check_sparta_sel(res, world, golden_dir, kind="random", device="cpu", rank_seeds=False):
     import strategy_scenarios as S
     nt = len(S.SEL_SHAPES)
+    # the draw that ran, as the strategy's __config__ records it (no silent fallback)
+    want_draw = "philox" if kind == "philox" else ("fused" if kind == "random" and device != "cpu" else "torch")
+    for r in range(world):
+        assert str(res[r]["mask_draw_0"]) == want_draw, (r, str(res[r]["mask_draw_0"]), want_draw)
     if kind == "random" and "gen_0" in res[0]:  # every rank's generator advanced by its own draws
         draws = S.SEL_STEPS * (nt - 1)
         for r in range(world):
@@ -159,17 +163,23 @@ def check_mnist_diloco(res, world, golden_dir):
     assert outer == 2
 
 
-def check_fedavg(res, world, golden_dir, island_size=None):
-    """Two averaging steps (rank 0's island draws from random.seed(1234)): every
+def check_fedavg(res, world, golden_dir, island_size=None, max_groups=None):
+    """Averaging steps (rank 0's island draws from random.seed(1234)): every
     node ends at the ascending-rank fp32 mean of its island, bit-exact (the
-    reference's sum(island_tensors) / len, federated_averaging.py:61-69)."""
+    reference's sum(island_tensors) / len, federated_averaging.py:61-69),
+    whether the round ran in cached island sub-communicators or in the world
+    all-gather; the sub-communicator cache stays within its bound."""
     nt = 3
+    rounds = int(res[0]["rounds"])
+    if max_groups is not None:
+        for r in range(world):
+            assert int(res[r]["ngroups"].max()) <= max_groups, res[r]["ngroups"]
     state = [[res[r][f"before_{i}"] for i in range(nt)] for r in range(world)]
     for r in range(world):
         for i in range(nt):
             assert np.array_equal(res[r][f"after0_{i}"], state[r][i])  # local_step 0: no averaging
     rng = random.Random(1234)
-    for step in (1, 2):
+    for step in range(1, rounds + 1):
         if island_size is None or island_size >= world:
             islands = [set(range(world))]
         else:

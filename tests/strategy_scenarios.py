@@ -182,6 +182,7 @@ def sc_sparta_sel(rank, world, dev, golden_dir, kind="random", rank_seeds=False)
         s.step()
         out[f"after_{step}"] = [_host(p) for p in model.parameters()]
     s.finish()
+    out["mask_draw"] = [np.array(str(s.__config__().get("mask_draw")))]
     if kind == "philox":
         out["seed"] = [np.array(comm._seed, dtype=np.int64)]
         out["offsets"] = [np.array(s.arena.layout.offsets, dtype=np.int64)]
@@ -248,8 +249,11 @@ def sc_mnist_diloco(rank, world, dev, golden_dir, steps=5, H=2):
     return out
 
 
-def sc_fedavg(rank, world, dev, golden_dir, island_size=None):
+def sc_fedavg(rank, world, dev, golden_dir, island_size=None, rounds=2, max_groups=None):
+    import gym_amd.strategy.federated_averaging as fa
     from gym_amd.strategy import FedAvgStrategy, OptimSpec
+    if max_groups is not None:  # bound the island sub-communicator cache
+        fa.MAX_ISLAND_GROUPS = max_groups
     shapes = [(66, 32), (128,), (3, 7)]
     model = ShapeModel(shapes, seed=500 + rank).to(dev)
     random.seed(1234)  # rank 0's island shuffle (the reference leaves `random` unseeded)
@@ -259,13 +263,16 @@ def sc_fedavg(rank, world, dev, golden_dir, island_size=None):
     s.zero_grad()
     s.step()  # local_step 0: no communication
     out["after0"] = [_host(p) for p in model.parameters()]
-    s.zero_grad()
-    s.step()  # local_step 1: average
-    out["after1"] = [_host(p) for p in model.parameters()]
-    s.zero_grad()
-    s.step()  # local_step 2: average again (new islands: new or cached sub-communicators)
-    out["after2"] = [_host(p) for p in model.parameters()]
-    return {f"{k}_{i}": v for k, lst in out.items() for i, v in enumerate(lst)}
+    ngroups = []
+    for step in range(1, rounds + 1):  # average every step (new islands: new or cached sub-communicators)
+        s.zero_grad()
+        s.step()
+        out[f"after{step}"] = [_host(p) for p in model.parameters()]
+        ngroups.append(len(s.communication_modules[0]._groups))
+    res = {f"{k}_{i}": v for k, lst in out.items() for i, v in enumerate(lst)}
+    res["ngroups"] = np.array(ngroups)
+    res["rounds"] = np.array(rounds)
+    return res
 
 
 def sc_demo(rank, world, dev, golden_dir):

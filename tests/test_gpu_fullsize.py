@@ -170,7 +170,7 @@ def test_demo_gpt2_350m_sampled_chunks():
         kk = max(1, min(32, n1 * n2))
         gy, gxc = R // n1, C // n2
         x2 = (np.float32(lr) * G0[off:off + nel]).reshape(R, C)  # delta = 0: x = RN(lr * g)
-        for cidx in rng.choice(gy * gxc, min(24, gy * gxc), replace=False):
+        for cidx in rng.choice(gy * gxc, min(256, gy * gxc), replace=False):
             y, xx = divmod(int(cidx), gxc)
             xc = x2[y * n1:(y + 1) * n1, xx * n2:(xx + 1) * n2]
             Y = odemo.encode(xc, (n1, n2), 64)
@@ -185,7 +185,7 @@ def test_demo_gpt2_350m_sampled_chunks():
                 Ym = np.zeros(n1 * n2)
                 Ym[oidx.reshape(-1)] = oval.reshape(-1)
                 R_ = odemo.decode(Ym.reshape(1, 1, n1, n2), (n1, n2), 64)
-                np.testing.assert_allclose(dchunk, xc - R_, rtol=0, atol=1e-5 * np.abs(xc).max())
+                np.testing.assert_allclose(dchunk, xc - R_, rtol=0, atol=1e-6 * np.abs(xc).max())
                 # decode of the own payload: p -= lr * sign(IDCT(top-k)), grad = the sign
                 sg = np.sign(R_)
                 gs = gS[off:off + nel].reshape(R, C)[y * n1:(y + 1) * n1, xx * n2:(xx + 1) * n2]
@@ -196,7 +196,7 @@ def test_demo_gpt2_350m_sampled_chunks():
                 np.testing.assert_allclose(pg[ok], (p0 - np.float32(lr) * sg)[ok], rtol=0, atol=1e-7)
                 checked += 1
         e0 += ne
-    assert checked > 50
+    assert checked > 500
     tally.done()
 
 

@@ -543,10 +543,10 @@ def test_demo_matches_reference_golden_steps(golden):
                         what=f"step {step} tensor {i}")
             ok = s == ref_s
             np.testing.assert_allclose(host(L.views(P[0])[i])[ok], z[f"p_after_{step}_{i}"][ok], rtol=0, atol=1e-6)
-            for k in range(K):
-                ref_d = z[f"delta_after_{step}_{i}"][k]
-                scale = max(np.abs(ref_d).max(), lr * np.abs(z[f"grad_{step}_{i}"][k]).max())
-                np.testing.assert_allclose(host(L.views(D[k])[i]), ref_d, rtol=0, atol=2e-5 * scale)
+            for k in range(K):  # 1e-6 x the chunk's scale wherever the node's top-k set is firm
+                x = decay * z[f"delta_before_{step}_{i}"][k].astype(np.float64) + lr * z[f"grad_{step}_{i}"][k]
+                demo_checks.residual_close(host(L.views(D[k])[i]), z[f"delta_after_{step}_{i}"][k], x, margins[k],
+                                           shapes[i], int(z["chunk"]), what=f"step {step} tensor {i} node {k}")
     tally.done()
 
 

@@ -92,7 +92,7 @@ def test_fit_returns_the_node_average_with_bn_buffers(name):
     ds = tiny_models.dataset()
     tr = LocalTrainer(model, ds, ds, start_port=21100 + 7 * ["simple", "diloco"].index(name))
     final = tr.fit(num_epochs=1, strategy=_strategies()[name], num_nodes=2, max_steps=5, device="cuda",
-                   batch_size=32, minibatch_size=16, val_size=32, val_interval=100)
+                   batch_size=32, minibatch_size=16, val_size=32, val_interval=100, keep_node_states=True)
     nodes = [_np_state(sd) for sd in tr.node_states]
     assert len(nodes) == 2
     assert not np.array_equal(nodes[0]["bn.running_mean"], nodes[1]["bn.running_mean"])  # nodes differ

@@ -24,6 +24,10 @@ CASES = [
     ("mnist_diloco", 2, {}),
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}), ("fedavg", 4, {"island_size": 2}),
     ("fedavg", 4, {"island_size": 3}),
+    # many rounds: C(4, 2) = 6 sets > 2 -> world all-gather every round, no group created;
+    # C(5, 2) + remainder at a cap of 8: groups until the cache is full, then the world path
+    ("fedavg", 4, {"island_size": 2, "rounds": 12, "max_groups": 2}),
+    ("fedavg", 5, {"island_size": 2, "rounds": 12, "max_groups": 12}),
     ("demo", 2, {}), ("demo_pipe", 2, {}), ("demo_pipe", 3, {"pieces": 2}),
 ]
 
@@ -31,7 +35,7 @@ CASES = [
 @pytest.mark.parametrize("name,world,kw", CASES, ids=[f"{c[0]}-w{c[1]}-{c[2]}" for c in CASES])
 def test_strategy_orchestration_gloo(tmp_path, name, world, kw):
     res = S.run(name, world, "cpu", True, str(tmp_path), GOLDEN, **kw)
-    check_kw = {k: kw[k] for k in ("island_size", "kind", "rank_seeds") if k in kw}
+    check_kw = {k: kw[k] for k in ("island_size", "kind", "rank_seeds", "max_groups") if k in kw}
     if name == "sparta_sel":
         check_kw["device"] = "cpu"
     CHECKS[name](res, world, GOLDEN, **check_kw)
