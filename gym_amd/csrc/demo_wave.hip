@@ -138,11 +138,14 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, int j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, j);
 }
 
-struct WaveLDS {
+struct ListLDS {
     uint32_t lst[2 * (kCand + 64)];  // candidates (pos, bits); slots kCand + lane: discard
     uint32_t bm[128];                // 4096-bit position bitmap
     uint32_t sm[4];                  // 128-bit rank-space selection mask
-    float tile[64 * kLd];            // row groups: T, then the masked coefficients
+};
+
+struct WaveLDS : ListLDS {
+    float tile[64 * kLd];  // 64x64 chunks: x, then delta (float4 t4 layout); row groups: T, then the masked coefficients
 };
 
 // ---- operands in registers --------------------------------------------------
@@ -396,96 +399,17 @@ __device__ __forceinline__ void store_coal(T* pb, int stride, bool vec, int lane
 __device__ __forceinline__ int t4(int row, int cb) { return row * 16 + (cb ^ (row & 15)); }
 
 
+// top-k of the chunk's coefficients Y (register t = 32 par + 16 qc + r: coefficient
+// b = 2 rowmap(r, h) + par, d = 2 l + qc), the payload, the residual delta = x - R in
+// the tile (x in the float4 t4 layout) and the coalesced delta store
 template <typename T>
-__device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* param, const T* grad, T* delta,
-                                        int32_t* out_idx, float* out_val, float lr, float decay, float wd_factor,
-                                        int ptr_vec, const float* Hb, WaveLDS& W
+__device__ __forceinline__ void chunk64_tail(const f32x16 (&Y)[2][2], int k, T* delta, int cols, bool vec,
+                                             int32_t* out_idx, float* out_val, const float* Hb, ListLDS& W,
+                                             float4* tile
 #ifdef GA_DEMO_STAMPS
-                                        , unsigned long long (&ph_acc)[16], unsigned long long& ph_last
+                                             , unsigned long long (&ph_acc)[16], unsigned long long& ph_last
 #endif
 ) {
-    const int k = td.k;
-    const int cy = c / td.gx, cx = c - cy * td.gx;
-    const int64_t base = td.offset + (int64_t)cy * 64 * td.cols + (int64_t)cx * 64;
-    param += base;
-    grad += base;
-    delta += base;
-    const bool vec = ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0);
-    float4* tile = reinterpret_cast<float4*>(W.tile);  // x, then delta, in the swizzled row-major layout
-    {
-        const int lane = lane_id();
-        if (wd_factor != 1.f) {  // decoupled weight decay of p (demo.py:159-160), its own pass
-            float pv[16][4];
-            load_coal(param, td.cols, vec, lane, pv);
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) pv[i][e] *= wd_factor;
-            store_coal(param, td.cols, vec, lane, pv);
-        }
-    }
-    f32x16 Y[2][2];  // [parity of b][qc]
-    {
-        // rows 0-31 (row-quads 0-7) are loaded ahead of rows 32-63, so the first
-        // half's row product runs while the second half is still in flight (the
-        // chunk's loads go out at raised priority, ahead of the partner wave's
-        // transforms; the products themselves stay at priority 0)
-        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-        float Dv[16][4], Gv[16][4];
-        __builtin_amdgcn_s_setprio(2);
-        load_coal<T, 0, 8>(delta, td.cols, vec, lane, Dv);
-        load_coal<T, 0, 8>(grad, td.cols, vec, lane, Gv);
-        __builtin_amdgcn_sched_barrier(0);  // issue order = vmcnt order: first half first
-        load_coal<T, 8, 8>(delta, td.cols, vec, lane, Dv);
-        load_coal<T, 8, 8>(grad, td.cols, vec, lane, Gv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)  // the first half is consumed only after every load is out
-            asm volatile("" : "+v"(Dv[i][0]), "+v"(Dv[i][1]), "+v"(Dv[i][2]), "+v"(Dv[i][3]), "+v"(Gv[i][0]),
-                              "+v"(Gv[i][1]), "+v"(Gv[i][2]), "+v"(Gv[i][3])::"memory");
-        __builtin_amdgcn_s_setprio(0);
-        f32x16 Tm[2][2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-#pragma unroll
-            for (int i = 8 * s; i < 8 * s + 8; ++i) {
-                if (s == 1)  // the second half's values materialise here, behind the first half's MFMAs
-                    asm volatile("" : "+v"(Dv[i][0]), "+v"(Dv[i][1]), "+v"(Dv[i][2]), "+v"(Dv[i][3]),
-                                      "+v"(Gv[i][0]), "+v"(Gv[i][1]), "+v"(Gv[i][2]), "+v"(Gv[i][3]));
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = fmaf(lr, Gv[i][e], Dv[i][e] * decay);  // * 1.0f is exact
-                tile[t4((lane >> 4) + 4 * i, lane & 15)] = make_float4(v[0], v[1], v[2], v[3]);
-            }
-            WAVE_LDS_SYNC();
-            float xs[8][4];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const float4 v = tile[t4(s ? 63 - l : l, blk(h, q))];
-                xs[q][0] = v.x;
-                xs[q][1] = v.y;
-                xs[q][2] = v.z;
-                xs[q][3] = v.w;
-            }
-            row_product_half(xs, Hb, l, h, Tm[s]);
-            // keep the first half's MFMAs ahead of the second half's loads' uses
-            if (s == 0) __builtin_amdgcn_sched_barrier(0);
-        }
-        DW_PH(1);
-#pragma unroll
-        for (int qc = 0; qc < 2; ++qc) {
-#pragma unroll
-            for (int par = 0; par < 2; ++par) {
-                f32x16 acc = zero16();
-#pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const float u = Tm[0][qc][t], w = Tm[1][qc][t];
-                    acc = mfma(Hb[rowmap(t, h) * kLd + 2 * l + par], par ? u - w : u + w, acc);
-                }
-                Y[par][qc] = acc;
-            }
-        }
-    }
-    DW_PH(2);
     // ---- top-k: register t = 32 par + 16 qc + r holds coefficient
     //      b = 2 rowmap(r, h) + par, d = 2 l + qc
     const int lane = lane_id(), l = lane & 31, h = lane >> 5;
@@ -736,10 +660,106 @@ __device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* para
             o[i][2] = v.z;
             o[i][3] = v.w;
         }
-        store_coal(delta, td.cols, vec, lane, o);
+        store_coal(delta, cols, vec, lane, o);
     }
     WAVE_LDS_SYNC();
     DW_PH(5);
+}
+
+template <typename T>
+__device__ __forceinline__ void chunk64(const ga_demo_tensor& td, int c, T* param, const T* grad, T* delta,
+                                        int32_t* out_idx, float* out_val, float lr, float decay, float wd_factor,
+                                        int ptr_vec, const float* Hb, WaveLDS& W
+#ifdef GA_DEMO_STAMPS
+                                        , unsigned long long (&ph_acc)[16], unsigned long long& ph_last
+#endif
+) {
+    const int cy = c / td.gx, cx = c - cy * td.gx;
+    const int64_t base = td.offset + (int64_t)cy * 64 * td.cols + (int64_t)cx * 64;
+    param += base;
+    grad += base;
+    delta += base;
+    const bool vec = ptr_vec && (td.offset % 4 == 0) && (td.cols % 4 == 0);
+    float4* tile = reinterpret_cast<float4*>(W.tile);  // x, then delta, in the swizzled row-major layout
+    {
+        const int lane = lane_id();
+        if (wd_factor != 1.f) {  // decoupled weight decay of p (demo.py:159-160), its own pass
+            float pv[16][4];
+            load_coal(param, td.cols, vec, lane, pv);
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pv[i][e] *= wd_factor;
+            store_coal(param, td.cols, vec, lane, pv);
+        }
+    }
+    f32x16 Y[2][2];  // [parity of b][qc]
+    {
+        // rows 0-31 (row-quads 0-7) are loaded ahead of rows 32-63, so the first
+        // half's row product runs while the second half is still in flight (the
+        // chunk's loads go out at raised priority, ahead of the partner wave's
+        // transforms; the products themselves stay at priority 0)
+        const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+        float Dv[16][4], Gv[16][4];
+        __builtin_amdgcn_s_setprio(2);
+        load_coal<T, 0, 8>(delta, td.cols, vec, lane, Dv);
+        load_coal<T, 0, 8>(grad, td.cols, vec, lane, Gv);
+        __builtin_amdgcn_sched_barrier(0);  // issue order = vmcnt order: first half first
+        load_coal<T, 8, 8>(delta, td.cols, vec, lane, Dv);
+        load_coal<T, 8, 8>(grad, td.cols, vec, lane, Gv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)  // the first half is consumed only after every load is out
+            asm volatile("" : "+v"(Dv[i][0]), "+v"(Dv[i][1]), "+v"(Dv[i][2]), "+v"(Dv[i][3]), "+v"(Gv[i][0]),
+                              "+v"(Gv[i][1]), "+v"(Gv[i][2]), "+v"(Gv[i][3])::"memory");
+        __builtin_amdgcn_s_setprio(0);
+        f32x16 Tm[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int i = 8 * s; i < 8 * s + 8; ++i) {
+                if (s == 1)  // the second half's values materialise here, behind the first half's MFMAs
+                    asm volatile("" : "+v"(Dv[i][0]), "+v"(Dv[i][1]), "+v"(Dv[i][2]), "+v"(Dv[i][3]),
+                                      "+v"(Gv[i][0]), "+v"(Gv[i][1]), "+v"(Gv[i][2]), "+v"(Gv[i][3]));
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = fmaf(lr, Gv[i][e], Dv[i][e] * decay);  // * 1.0f is exact
+                tile[t4((lane >> 4) + 4 * i, lane & 15)] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+            WAVE_LDS_SYNC();
+            float xs[8][4];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const float4 v = tile[t4(s ? 63 - l : l, blk(h, q))];
+                xs[q][0] = v.x;
+                xs[q][1] = v.y;
+                xs[q][2] = v.z;
+                xs[q][3] = v.w;
+            }
+            row_product_half(xs, Hb, l, h, Tm[s]);
+            // keep the first half's MFMAs ahead of the second half's loads' uses
+            if (s == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        DW_PH(1);
+#pragma unroll
+        for (int qc = 0; qc < 2; ++qc) {
+#pragma unroll
+            for (int par = 0; par < 2; ++par) {
+                f32x16 acc = zero16();
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const float u = Tm[0][qc][t], w = Tm[1][qc][t];
+                    acc = mfma(Hb[rowmap(t, h) * kLd + 2 * l + par], par ? u - w : u + w, acc);
+                }
+                Y[par][qc] = acc;
+            }
+        }
+    }
+    DW_PH(2);
+    chunk64_tail<T>(Y, td.k, delta, td.cols, vec, out_idx, out_val, Hb, W, tile
+#ifdef GA_DEMO_STAMPS
+                    , ph_acc, ph_last
+#endif
+    );
 }
 
 // ---- row group: up to 64 consecutive 1x64 chunks (F1 = [1]) ---------------

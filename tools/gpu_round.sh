@@ -9,6 +9,8 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "SMOKE FAILED"; tail -30 $O/smoke.log; exit 1; }
+cat $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pmc > $O/prof.log 2>&1 || { echo "PROF FAILED"; tail -20 $O/prof.log; exit 1; }
