@@ -38,6 +38,7 @@ constexpr int kWaves = 8;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kLd = 65;     // LDS row stride (basis, row-group tile)
 constexpr int kCand = 128;  // fast-path candidate capacity
+static_assert(2 * (kCand + 64) >= 320, "the fallback top-k keeps its maps in lst[128..319]");
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -541,84 +542,121 @@ __device__ __forceinline__ void chunk64_tail(const f32x16 (&Y)[2][2], int k, T* 
         }
         WAVE_LDS_SYNC();
     } else {
+#ifdef GA_EXP_NOFALLBACK
+        __builtin_trap();
+    }
+    if (0) {
+#endif
         // more than kCand keys >= T0 (flat spectra, all-zero chunks): exact k-th
-        // key over all 4096 keys, ties to the lowest positions, slots in position order
+        // key over all 4096 keys, ties to the lowest positions, slots in position order.
+        // Rare, so written for registers, not speed: every loop re-reads Y through an
+        // opaque copy and rebuilds positions from an opaque lane base (nothing derived
+        // from the 64 coefficients stays live across loops), and the tie ranks come
+        // from LDS (bitmap words + per-word prefix counts at lst[128..191]).
         DW_CNT(8);
+        auto opq = [](float v) {
+            asm volatile("" : "+v"(v));
+            return v;
+        };
+        auto lane_pos = [&]() {  // p = lp + (2 ((r & 3) + 8 (r >> 2)) + par) * 64 + qc
+            uint32_t lp = (uint32_t)(512 * h + 2 * l);
+            asm volatile("" : "+v"(lp));
+            return lp;
+        };
+        auto pos_c = [](int par, int qc, int r) -> uint32_t {
+            return (uint32_t)((2 * ((r & 3) + 8 * (r >> 2)) + par) * 64 + qc);
+        };
         uint32_t thr = 0;
         for (int bit = 31; bit >= 0; --bit) {
             const uint32_t cnd = thr | (1u << bit);
+            const float f = __uint_as_float(cnd - 1u);
             int cl = 0;
 #pragma unroll
             for (int par = 0; par < 2; ++par)
 #pragma unroll
                 for (int qc = 0; qc < 2; ++qc)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) cl += fabsf(Y[par][qc][r]) >= __uint_as_float(cnd - 1u) ? 1 : 0;
+                    for (int r = 0; r < 16; ++r) cl += fabsf(opq(Y[par][qc][r])) >= f ? 1 : 0;
             if (wave_sum(cl) >= k) thr = cnd;
         }
         int gl = 0;
+        {
+            const uint32_t lp = lane_pos();
 #pragma unroll
-        for (int par = 0; par < 2; ++par)
+            for (int par = 0; par < 2; ++par)
 #pragma unroll
-            for (int qc = 0; qc < 2; ++qc)
+                for (int qc = 0; qc < 2; ++qc)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const uint32_t kv = keyv(Y[par][qc][r]);
-                    gl += kv > thr ? 1 : 0;
-                    if (kv == thr) {
-                        const uint32_t p = posof(par, qc, r);
-                        atomicOr(&W.bm[p >> 5], 1u << (p & 31));
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t kv = keyv(opq(Y[par][qc][r]));
+                        gl += kv > thr ? 1 : 0;
+                        if (kv == thr) {
+                            const uint32_t p = lp + pos_c(par, qc, r);
+                            atomicOr(&W.bm[p >> 5], 1u << (p & 31));
+                        }
                     }
-                }
+        }
         const int need = k - wave_sum(gl);
         WAVE_LDS_SYNC();
-        uint32_t w0 = W.bm[2 * lane], w1 = W.bm[2 * lane + 1];
-        int cnt = __popc(w0) + __popc(w1);
-        int pre = wave_excl_scan128(cnt);
+        uint32_t* preL = W.lst + 128;  // per 64-position word pair: tied positions before it
+        {
+            const uint32_t w0 = W.bm[2 * lane], w1 = W.bm[2 * lane + 1];
+            preL[lane] = (uint32_t)wave_excl_scan128(__popc(w0) + __popc(w1));
+        }
         WAVE_LDS_SYNC();
-        W.bm[2 * lane] = 0u;  // becomes the selection bitmap
-        W.bm[2 * lane + 1] = 0u;
+        // a tied coefficient's tie rank = tied positions below it; the selection goes to
+        // a second 4096-bit map at lst[192..319] (the entries written below use lst[0..2k))
+        uint32_t* sel = W.lst + 192;
+        sel[2 * lane] = 0u;
+        sel[2 * lane + 1] = 0u;
         WAVE_LDS_SYNC();
-        // a tied coefficient's tie rank = tied positions below it
+        {
+            const uint32_t lp = lane_pos();
 #pragma unroll
-        for (int par = 0; par < 2; ++par)
+            for (int par = 0; par < 2; ++par)
 #pragma unroll
-            for (int qc = 0; qc < 2; ++qc)
+                for (int qc = 0; qc < 2; ++qc)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const uint32_t kv = keyv(Y[par][qc][r]);
-                    const uint32_t p = posof(par, qc, r);
-                    const int Lw = (int)(p >> 6);
-                    const uint64_t pair = ((uint64_t)(uint32_t)__shfl((int)w1, Lw, 64) << 32) |
-                                          (uint32_t)__shfl((int)w0, Lw, 64);
-                    const int tr = __shfl(pre, Lw, 64) + __popcll(pair & ((1ull << (p & 63)) - 1ull));
-                    if (kv > thr || (kv == thr && tr < need)) atomicOr(&W.bm[p >> 5], 1u << (p & 31));
-                }
-        WAVE_LDS_SYNC();
-        w0 = W.bm[2 * lane];
-        w1 = W.bm[2 * lane + 1];
-        cnt = __popc(w0) + __popc(w1);
-        pre = wave_excl_scan128(cnt);
-#pragma unroll
-        for (int par = 0; par < 2; ++par)
-#pragma unroll
-            for (int qc = 0; qc < 2; ++qc)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const uint32_t p = posof(par, qc, r);
-                    const int Lw = (int)(p >> 6);
-                    const uint64_t pair = ((uint64_t)(uint32_t)__shfl((int)w1, Lw, 64) << 32) |
-                                          (uint32_t)__shfl((int)w0, Lw, 64);
-                    const int preL = __shfl(pre, Lw, 64);
-                    if ((pair >> (p & 63)) & 1ull) {
-                        const int slot = preL + __popcll(pair & ((1ull << (p & 63)) - 1ull));
-                        const float v = Y[par][qc][r];
-                        W.lst[2 * slot] = p;
-                        W.lst[2 * slot + 1] = __float_as_uint(v);
-                        out_idx[slot] = (int32_t)p;
-                        out_val[slot] = v;
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t kv = keyv(opq(Y[par][qc][r]));
+                        const uint32_t p = lp + pos_c(par, qc, r);
+                        bool s = kv > thr;
+                        if (kv == thr) {
+                            const uint32_t Lw = p >> 6;
+                            const uint64_t pair = ((uint64_t)W.bm[2 * Lw + 1] << 32) | W.bm[2 * Lw];
+                            const int tr = (int)preL[Lw] + __popcll(pair & ((1ull << (p & 63)) - 1ull));
+                            s = tr < need;
+                        }
+                        if (s) atomicOr(&sel[p >> 5], 1u << (p & 31));
                     }
-                }
+        }
+        WAVE_LDS_SYNC();
+        {
+            const uint32_t w0 = sel[2 * lane], w1 = sel[2 * lane + 1];
+            preL[lane] = (uint32_t)wave_excl_scan128(__popc(w0) + __popc(w1));
+        }
+        WAVE_LDS_SYNC();
+        {
+            const uint32_t lp = lane_pos();
+#pragma unroll
+            for (int par = 0; par < 2; ++par)
+#pragma unroll
+                for (int qc = 0; qc < 2; ++qc)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t p = lp + pos_c(par, qc, r);
+                        const uint32_t Lw = p >> 6;
+                        const uint64_t pair = ((uint64_t)sel[2 * Lw + 1] << 32) | sel[2 * Lw];
+                        if ((pair >> (p & 63)) & 1ull) {
+                            const int slot = (int)preL[Lw] + __popcll(pair & ((1ull << (p & 63)) - 1ull));
+                            const float v = opq(Y[par][qc][r]);
+                            W.lst[2 * slot] = p;  // slot < k <= 64: below lst[128]
+                            W.lst[2 * slot + 1] = __float_as_uint(v);
+                            out_idx[slot] = (int32_t)p;
+                            out_val[slot] = v;
+                        }
+                    }
+        }
         WAVE_LDS_SYNC();
     }
     DW_PH(3);
@@ -921,18 +959,230 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
     DW_PH_FLUSH();
 }
 
+// ============================================================================
+// Encode, loader / consumer form: the 64x64 chunks of ga_demo_encode_sym.
+//
+// A workgroup of 12 waves per CU (3 per SIMD, <= 168 VGPRs each): 8 CONSUMER
+// waves transform chunks, 4 LOADER waves stream them in.  Loader w feeds
+// consumers w and w + 4 alternately: it loads a chunk's delta and grad
+// (coalesced, 32 KB in registers), forms x = decay * delta + lr * grad, waits
+// for the consumer's LDS slot to be free and writes x into it (the swizzled t4
+// layout).  The consumer never waits on HBM: it reads x from its slot in the
+// row-pair layout, runs both DCT products, the top-k and the residual, leaves
+// delta = x - R in the slot, stores it coalesced and frees the slot.  So the
+// matrix and vector pipes of a SIMD serve two consumers while its loader keeps
+// the next chunk's loads in flight -- instead of every wave alternating
+// between waiting on its own loads and computing (the all-in-one kernel
+// above, two waves per SIMD).
+// Hand-off: one LDS word per slot, 2i + 1 = chunk i written, 2i + 2 = chunk i
+// consumed (0 initially); a wave's LDS operations execute in order, so a word
+// written after the data is seen only after the data.
+// The arithmetic per chunk is chunk64's (same x rounding, same products, same
+// top-k and residual), so the results are identical to the all-in-one kernel.
+// ============================================================================
+__device__ __forceinline__ int64_t chunk_base(const ga_demo_tensor& td, int c);
+__device__ __forceinline__ bool chunk_vec(const ga_demo_tensor& td, int ptr_vec);
+
+constexpr int kCons = 8;
+constexpr int kLoaders = 4;
+constexpr int kLcThreads = 64 * (kCons + kLoaders);
+
+struct LcLDS {
+    float Hb[32 * kLd];
+    float4 slot[kCons][64 * 16];
+    ListLDS lists[kCons];
+    int flag[kCons];
+};
+
+__device__ __forceinline__ void lds_wait_flag(const int* f, int want) {
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != want) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void lds_set_flag(int* f, int v) {
+    asm volatile("" ::: "memory");
+    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// A wave's chunk sequence job0, job0 + stride, ... as (replica, chunk) pairs, advanced
+// with scalar arithmetic (no 64-bit division per chunk)
+struct LcCursor {
+    int64_t rep;
+    int chunk;
+    __device__ __forceinline__ LcCursor(int64_t job, int nchunks) {
+        rep = job / nchunks;
+        chunk = (int)(job - rep * nchunks);
+    }
+    __device__ __forceinline__ void advance(int64_t stride, int nchunks) {
+        const int64_t r = stride / nchunks;  // uniform; stride < nchunks in practice
+        rep += r;
+        chunk += (int)(stride - r * nchunks);
+        if (chunk >= nchunks) {
+            chunk -= nchunks;
+            ++rep;
+        }
+    }
+};
+
+struct LcJob {
+    ga_demo_tensor td;
+    int c;         // chunk within the tensor
+    int64_t base;  // element offset of the chunk's (0, 0) in its replica
+    bool vec;
+};
+
+__device__ __forceinline__ LcJob lc_job(const ga_demo_tensor* __restrict__ tens, int ntens, int chunk, int ptr_vec) {
+    LcJob j;
+    j.td = tens[find_tensor(tens, ntens, -1, chunk)];
+    j.c = chunk - j.td.chunk_start;
+    j.base = chunk_base(j.td, j.c);
+    j.vec = chunk_vec(j.td, ptr_vec);
+    return j;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kLcThreads) void encode_lc_kernel(
+    const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const float* __restrict__ F64, T* param0,
+    const T* __restrict__ grad0, T* delta0, int64_t ld, int64_t K, float lr, float decay, float wd_factor,
+    int32_t* payload0, int64_t pstride, int64_t M, int ptr_vec) {
+    __shared__ LcLDS L;
+    for (int q = threadIdx.x; q < 32 * 64; q += kLcThreads) L.Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
+    if (threadIdx.x < kCons) L.flag[threadIdx.x] = 0;
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int64_t n64 = (int64_t)nchunks * K;
+    const int64_t stride = (int64_t)gridDim.x * kCons;
+    if (wid < kCons) {  // ---- consumer
+        const int cw = wid;
+        float4* tile = L.slot[cw];
+        int i = 0;
+        LcCursor cur((int64_t)blockIdx.x * kCons + cw, nchunks);
+        for (int64_t job = (int64_t)blockIdx.x * kCons + cw; job < n64; job += stride, ++i, cur.advance(stride, nchunks)) {
+            const LcJob j = lc_job(tens, ntens, cur.chunk, ptr_vec);
+            const int64_t rep = cur.rep;
+            int32_t* pi = payload0 + rep * pstride + j.td.payload_off + (int64_t)j.c * j.td.k;
+            float* pv = reinterpret_cast<float*>(payload0 + rep * pstride + M) + j.td.payload_off + (int64_t)j.c * j.td.k;
+            lds_wait_flag(&L.flag[cw], 2 * i + 1);
+            const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+            f32x16 Y[2][2];  // [parity of b][qc]
+            {
+                f32x16 Tm[2][2];
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    float xs[8][4];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float4 v = tile[t4(s2 ? 63 - l : l, blk(h, q))];
+                        xs[q][0] = v.x;
+                        xs[q][1] = v.y;
+                        xs[q][2] = v.z;
+                        xs[q][3] = v.w;
+                    }
+                    row_product_half(xs, L.Hb, l, h, Tm[s2]);
+                }
+#pragma unroll
+                for (int qc = 0; qc < 2; ++qc) {
+#pragma unroll
+                    for (int par = 0; par < 2; ++par) {
+                        f32x16 acc = zero16();
+#pragma unroll
+                        for (int t = 0; t < 16; ++t) {
+                            const float u = Tm[0][qc][t], w = Tm[1][qc][t];
+                            acc = mfma(L.Hb[rowmap(t, h) * kLd + 2 * l + par], par ? u - w : u + w, acc);
+                        }
+                        Y[par][qc] = acc;
+                    }
+                }
+            }
+#ifdef GA_DEMO_STAMPS
+            unsigned long long ph_acc[16] = {}, ph_last = 0;
+#endif
+            chunk64_tail<T>(Y, j.td.k, delta0 + rep * ld + j.base, j.td.cols, j.vec, pi, pv, L.Hb, L.lists[cw], tile
+#ifdef GA_DEMO_STAMPS
+                            , ph_acc, ph_last
+#endif
+            );
+            lds_set_flag(&L.flag[cw], 2 * i + 2);
+        }
+    } else {  // ---- loader: consumers lw and lw + kLoaders, alternately
+        const int lw = wid - kCons;
+        __builtin_amdgcn_s_setprio(1);
+        LcCursor curs[2] = {LcCursor((int64_t)blockIdx.x * kCons + lw, nchunks),
+                            LcCursor((int64_t)blockIdx.x * kCons + lw + kLoaders, nchunks)};
+        for (int i = 0;; ++i) {
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int cw = lw + u * kLoaders;
+                const int64_t job = (int64_t)blockIdx.x * kCons + cw + (int64_t)i * stride;
+                if (job >= n64) continue;
+                any = true;
+                const LcJob j = lc_job(tens, ntens, curs[u].chunk, ptr_vec);
+                const int64_t rep = curs[u].rep;
+                curs[u].advance(stride, nchunks);
+                const int lane = lane_id();
+                T* prm = param0 + rep * ld + j.base;
+                if (wd_factor != 1.f) {  // decoupled weight decay of p (demo.py:159-160), its own pass
+                    float pw[16][4];
+                    load_coal(prm, j.td.cols, j.vec, lane, pw);
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) pw[q][e] *= wd_factor;
+                    store_coal(prm, j.td.cols, j.vec, lane, pw);
+                }
+                float Dv[16][4], Gv[16][4];
+                load_coal(delta0 + rep * ld + j.base, j.td.cols, j.vec, lane, Dv);
+                load_coal(grad0 + rep * ld + j.base, j.td.cols, j.vec, lane, Gv);
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) Dv[q][e] = fmaf(lr, Gv[q][e], Dv[q][e] * decay);  // as chunk64
+                lds_wait_flag(&L.flag[cw], 2 * i);
+                float4* tile = L.slot[cw];
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    tile[t4((lane >> 4) + 4 * q, lane & 15)] = make_float4(Dv[q][0], Dv[q][1], Dv[q][2], Dv[q][3]);
+                lds_set_flag(&L.flag[cw], 2 * i + 1);
+            }
+            if (!any) break;
+        }
+    }
+}
+
+// GA_DEMO_ENCODE_LC=0 selects the all-in-one kernel for the 64x64 chunks too (A/B and
+// parity tests; read at every launch)
+static int lc_enabled() {
+    const char* e = getenv("GA_DEMO_ENCODE_LC");
+    return e && e[0] == '0' ? 0 : 1;
+}
+
 template <typename T>
 static int launch(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, const ga_demo_rowgroup* groups,
                   int32_t ngroups, const float* F64, void* param, const void* grad, void* delta, int64_t K,
                   int64_t ld, float lr, float decay, float wd_factor, int32_t* payload, int64_t pstride, int64_t M,
                   int ptr_vec, hipStream_t stream) {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n > 0 ? n : 256;
+    }();
+    const bool lc = lc_enabled() && nchunks > 0;
+    if (lc) {  // 64x64 chunks: loader / consumer kernel, one workgroup per CU
+        const int64_t want = ((int64_t)nchunks * K + kCons - 1) / kCons;
+        const int grid = (int)(want < cus ? want : cus);
+        hipLaunchKernelGGL(encode_lc_kernel<T>, dim3(grid), dim3(kLcThreads), 0, stream, tens, ntens, nchunks, F64,
+                           (T*)param, (const T*)grad, (T*)delta, ld, K, lr, decay, wd_factor, payload, pstride, M,
+                           ptr_vec);
+        if (ngroups == 0) return GA_OK;
+        nchunks = 0;  // the row groups: the all-in-one kernel below
+    }
     auto kern = encode_kernel<T>;
     static const int resident = [&] {
-        int per_cu = 0, dev = 0, cus = 0;
+        int per_cu = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0);
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
+        return (per_cu > 0 ? per_cu : 1) * cus;
     }();
     const int64_t jobs = ((int64_t)nchunks + ngroups) * K;
     const int64_t want = (jobs + kWaves - 1) / kWaves;

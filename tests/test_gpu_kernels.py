@@ -1023,3 +1023,33 @@ def test_fused_draw_self_check():
     before = torch.cuda.get_rng_state()
     assert sp.fused_draw_matches_torch(DEV)
     assert torch.equal(torch.cuda.get_rng_state(), before)
+
+
+@pytest.mark.parametrize("K,zero_chunks", [(1, False), (3, True)])
+def test_demo_encode_loader_consumer_matches_all_in_one(monkeypatch, K, zero_chunks):
+    """ga_demo_encode_sym's loader/consumer kernel (the default for 64x64
+    chunks) against its all-in-one kernel (GA_DEMO_ENCODE_LC=0): the same
+    arithmetic per chunk, so payload, residual delta and weight-decayed params
+    are bit-identical -- over every GPT-2-like chunk kind, batched replicas,
+    and all-zero chunks (the > kCand top-k fallback)."""
+    from gym_amd import ops
+    shapes = [(192, 128), (768,), (64, 64), (128, 192), (320,), (64, 256), (1024, 64)]
+    L, plan, a = _demo_setup(shapes, K, seed=11 + K)
+    assert plan.wave_encode
+    if zero_chunks:  # tensor 0's second 64-row block and tensor 6's first chunk: delta = grad = 0
+        for k in range(K):
+            for arr in (a["g"], a["d"]):
+                v = arr[k, L.offsets[0]:L.offsets[0] + L.numels[0]].reshape(192, 128)
+                v[64:128] = 0
+                v2 = arr[k, L.offsets[6]:L.offsets[6] + L.numels[6]].reshape(1024, 64)
+                v2[:64] = 0
+    lr, decay, wdf = 0.01, 0.999, float(np.float32(1.0 - 0.01 * 0.1))
+    out = {}
+    for lc in ("0", "1"):
+        monkeypatch.setenv("GA_DEMO_ENCODE_LC", lc)
+        P, G, D = t(a["p"]), t(a["g"]), t(a["d"])
+        payload = torch.zeros(K, 2 * plan.M, dtype=torch.int32, device=DEV)
+        ops.demo_encode(plan, P, G, D, payload, lr, decay, wdf)
+        out[lc] = (host(P), host(D), payload.cpu().numpy())
+    for a0, a1, what in zip(out["0"], out["1"], ("p", "delta", "payload")):
+        assert np.array_equal(a0, a1), what
