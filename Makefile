@@ -7,7 +7,7 @@ OBJ := $(patsubst gym_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := gym_amd/_lib/libgym_amd.so
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -fvisibility=hidden -Wall -Wno-unused-function
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle asan
 all: $(LIB)
 
 build/%.o: gym_amd/csrc/%.hip gym_amd/csrc/ga_common.h include/gym_amd.h
@@ -32,3 +32,17 @@ stamps: $(STAMP_LIB)
 $(STAMP_LIB): $(SRC) gym_amd/csrc/ga_common.h include/gym_amd.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -DGA_DEMO_STAMPS -shared -o $@ $(SRC)
+
+# Host AddressSanitizer build of the C ABI: the argument validation and
+# host wrappers of every ga_* entry point instrumented (-Xarch_host: the device code is
+# built as usual; GPU sanitizers are not used).  tests/test_abi_asan.py loads it into a
+# python run with the ASan runtime preloaded and drives test_abi.py's invalid-argument
+# cases through it (no GPU needed).
+ASAN_LIB := build/libgym_amd_asan.so
+ASAN_RT := $(firstword $(wildcard /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so))
+asan: $(ASAN_LIB)
+$(ASAN_LIB): $(SRC) gym_amd/csrc/ga_common.h include/gym_amd.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer -shared-libsan \
+		-shared -o $@ $(SRC)
+	@echo "ASan runtime: $(ASAN_RT)"
