@@ -49,6 +49,10 @@ class RunLog:
     def increment_step(self):
         self.step += 1
 
+    def summary(self):
+        """Plain lists (picklable through the trainer's result queue)."""
+        return {"train": list(self.train), "evals": list(self.evals), "lrs": list(self.lrs)}
+
 
 class TrainNode(LogModule):
     def __init__(self, model: torch.nn.Module,

@@ -74,7 +74,8 @@ def _worker(rank: int, config: TrainingConfig, result_queue):
     for f in _FIELDS:
         setattr(trainer, f, getattr(config, f))
     state = trainer._fit_process(rank)
-    result_queue.put((rank, OrderedDict((k, v.detach().cpu()) for k, v in state.items())))
+    log = trainer.run_log.summary() if getattr(trainer, "run_log", None) is not None else None
+    result_queue.put((rank, OrderedDict((k, v.detach().cpu()) for k, v in state.items()), log))
 
 
 def _replica_worker(rank: int, config: TrainingConfig, procs: int, K: int, result_queue):
@@ -95,8 +96,10 @@ def _replica_worker(rank: int, config: TrainingConfig, procs: int, K: int, resul
                             autocast=trainer.autocast, **trainer.kwargs)
     states = node.train()
     trainer._process_cleanup()
+    log = node.logger.summary() if node.logger is not None else None
     for k, sd in enumerate(states):
-        result_queue.put((rank * K + k, OrderedDict((n, v.detach().cpu()) for n, v in sd.items())))
+        result_queue.put((rank * K + k, OrderedDict((n, v.detach().cpu()) for n, v in sd.items()),
+                          log if k == 0 else None))
 
 
 def _average_model_states(model_states: Dict[int, OrderedDict]) -> Optional[OrderedDict]:
@@ -161,9 +164,12 @@ class Trainer:
             procs, K = layout
             mp.spawn(_replica_worker, args=(config, procs, K, queue), nprocs=procs, start_method="spawn", join=True)
         states = {}
+        self.run_log = None  # rank 0's record: train losses, evaluation losses, learning rates
         for _ in range(num_nodes):
-            r, sd = queue.get()
+            r, sd, log = queue.get()
             states[r] = sd
+            if log is not None:
+                self.run_log = log
         self.node_states = [states[r] for r in sorted(states)] if keep_node_states else None
         avg = _average_model_states(states)
         if avg is None:
