@@ -1255,7 +1255,7 @@ __device__ __forceinline__ void store_quad(T* pb, int i, int stride, bool vec, i
 
 template <typename T>
 __device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, int stride, bool vec, float lr,
-                                            int lane, const PRaw<T>& raw) {
+                                            int lane, PRaw<T>& raw) {
     if constexpr (sizeof(typename Vec4<T>::type) < 16) {
         // packed (bf16) rows: widen, update and store one row quad at a time, so the
         // fp32 copy of the chunk is never live whole (244 -> 116 B/lane of spill at 8 sources)
@@ -1278,39 +1278,70 @@ __device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, in
                 store_quad(gr, i, stride, vec, lane, f);
             }
         }
-        return;
-    }
-    // fp32: every fused update first, then the 16 stores back to back (measured: the
-    // per-quad form above costs fp32 ~20% here)
-    float p[16][4];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
-        Vec4<T>::unpack(raw[i], p[i]);
-        p[i][0] = fmaf(-lr, v.x, p[i][0]);
-        p[i][1] = fmaf(-lr, v.y, p[i][1]);
-        p[i][2] = fmaf(-lr, v.z, p[i][2]);
-        p[i][3] = fmaf(-lr, v.w, p[i][3]);
-    }
-    store_coal(pr, stride, vec, lane, p);
-    if (gr) {
+    } else {
+        // fp32: every fused update first (in place, in the registers the parameters were
+        // loaded into), then the 16 stores back to back (measured: the per-quad form
+        // above costs fp32 ~20% here)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
-            p[i][0] = v.x;
-            p[i][1] = v.y;
-            p[i][2] = v.z;
-            p[i][3] = v.w;
+            raw[i].x = fmaf(-lr, v.x, raw[i].x);
+            raw[i].y = fmaf(-lr, v.y, raw[i].y);
+            raw[i].z = fmaf(-lr, v.z, raw[i].z);
+            raw[i].w = fmaf(-lr, v.w, raw[i].w);
         }
-        store_coal(gr, stride, vec, lane, p);
+        if (vec) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) *reinterpret_cast<float4*>(at_off(pr, coal_off(i, lane, stride))) = raw[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float f[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+                store_quad(pr, i, stride, vec, lane, f);
+            }
+        }
+        if (gr) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+                const float f[4] = {v.x, v.y, v.z, v.w};
+                store_quad(gr, i, stride, vec, lane, f);
+            }
+        }
     }
 }
 
 template <typename T>
 __device__ __forceinline__ void apply_signs(const float4* tile, T* param, T* grad, int64_t K, int64_t ld, int stride,
-                                            bool vec, int nrows, float lr, int lane, const PRaw<T>& pre) {
+                                            bool vec, int nrows, float lr, int lane, PRaw<T>& pre, bool lean = false) {
     if (nrows == 64) {
         sign_update(tile, param, grad, stride, vec, lr, lane, pre);
+        if (lean) {  // replicas 1.. a row quad at a time (the updater waves' register budget)
+            for (int64_t r = 1; r < K; ++r) {
+#pragma unroll 4
+                for (int i = 0; i < 16; ++i) {
+                    const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+                    T* a = at_off(param + r * ld, coal_off(i, lane, stride));
+                    float f[4];
+                    if (vec) {
+                        Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(a), f);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) f[e] = Elem<T>::load(a + e);
+                    }
+                    f[0] = fmaf(-lr, v.x, f[0]);
+                    f[1] = fmaf(-lr, v.y, f[1]);
+                    f[2] = fmaf(-lr, v.z, f[2]);
+                    f[3] = fmaf(-lr, v.w, f[3]);
+                    store_quad(param + r * ld, i, stride, vec, lane, f);
+                    if (grad) {
+                        const float g4[4] = {v.x, v.y, v.z, v.w};
+                        store_quad(grad + r * ld, i, stride, vec, lane, g4);
+                    }
+                }
+            }
+            return;
+        }
         for (int64_t r = 1; r < K; ++r) {
             PRaw<T> p;
             load_coal_raw(param + r * ld, stride, vec, lane, p);
@@ -1389,6 +1420,22 @@ __device__ __forceinline__ void dchunk_entries(const ga_demo_tensor& td, int c, 
                                                int64_t pstride, int64_t M, int S, DecIn<MS>& in) {
     const int k = td.k, lane = lane_id();
     const int64_t e0 = td.payload_off + (int64_t)c * k;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) {
+        in.xs[s] = -1;
+        in.vs[s] = 0.f;
+        if (s < S && lane < k) {
+            in.xs[s] = payload[(int64_t)s * pstride + e0 + lane];
+            in.vs[s] = reinterpret_cast<const float*>(payload + (int64_t)s * pstride + M)[e0 + lane];
+        }
+    }
+}
+
+// the same from a chunk's entry offset e0 and k
+template <int MS>
+__device__ __forceinline__ void dchunk_entries_at(int k, int64_t e0, const int32_t* __restrict__ payload,
+                                                  int64_t pstride, int64_t M, int S, DecIn<MS>& in) {
+    const int lane = lane_id();
 #pragma unroll
     for (int s = 0; s < MS; ++s) {
         in.xs[s] = -1;
@@ -1617,11 +1664,129 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     }
 }
 
+// ============================================================================
+// Decode, consumer / updater form (64x64 chunks, S <= 8 sources): the same
+// split as the encode's loader / consumer kernel.  Per workgroup (one per CU,
+// 12 waves, <= 168 VGPRs): 8 CONSUMER waves turn a chunk's gathered entries
+// into sign(g) in their LDS slot (dchunk_signs: scatter-mean + inverse DCT, the
+// next chunk's entries already in flight), 4 UPDATER waves, each serving
+// consumers u and u + 4, hold the replica-0 parameters of both consumers' next
+// chunks in registers (loaded a whole chunk ahead), wait for the signs, run
+// p -= lr * sign and grad = sign for every replica and free the slot.  The
+// consumers never wait on HBM; the updaters never wait on the transform while
+// there is a chunk to store.  Same per-chunk arithmetic as decode_kernel.
+// Slot words: 2i = free for chunk i, 2i + 1 = chunk i's signs written.
+// ============================================================================
+constexpr int kUpd = 4;
+
+struct DecLcLDS {
+    float Hb[32 * kLd];
+    DecLDS slot[kCons];
+    int flag[kCons];
+};
+
+template <typename T, int MS>
+__global__ __launch_bounds__(kLcThreads) void decode_lc_kernel(
+    const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const float* __restrict__ F64,
+    const int32_t* __restrict__ payload, int64_t pstride, int64_t M, int S, T* param, T* grad, int64_t K, int64_t ld,
+    float lr, int ptr_vec) {
+    static_assert(kCons + kUpd == kLcThreads / 64, "12 waves: 8 consumers, 4 updaters");
+    __shared__ DecLcLDS L;
+    for (int q = threadIdx.x; q < 32 * 64; q += kLcThreads) L.Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
+    if (threadIdx.x < kCons) L.flag[threadIdx.x] = 0;
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int64_t stride = (int64_t)gridDim.x * kCons;
+    if (wid < kCons) {  // ---- consumer
+        const int cw = wid;
+        DecLDS& W = L.slot[cw];
+        int64_t job = (int64_t)blockIdx.x * kCons + cw;
+        if (job >= nchunks) return;
+        // a chunk's entries start at e0 = payload_off + c * k of its tensor
+        auto entries_at = [&](int64_t j, int& k, int64_t& e0) {
+            const int t = find_tensor(tens, ntens, -1, (int)j);
+            k = tens[t].k;
+            e0 = tens[t].payload_off + (int64_t)((int)j - tens[t].chunk_start) * k;
+        };
+        int k;
+        int64_t e0;
+        entries_at(job, k, e0);
+        DecIn<MS> cur;
+        dchunk_entries_at<MS>(k, e0, payload, pstride, M, S, cur);
+        for (int i = 0;; ++i) {
+            const int64_t nj = job + stride;
+            const bool more = nj < nchunks;
+            int kn = k;
+            int64_t e0n = e0;
+            if (more) entries_at(nj, kn, e0n);
+            // the next chunk's entries, in flight behind this transform (none past the end:
+            // every slot is still written, so the struct stays in registers)
+            DecIn<MS> nxt;
+            dchunk_entries_at<MS>(kn, e0n, payload, pstride, M, more ? S : 0, nxt);
+            lds_wait_flag(&L.flag[cw], 2 * i);
+            dchunk_signs(k, S, cur, L.Hb, W);
+            lds_set_flag(&L.flag[cw], 2 * i + 1);
+            if (!more) break;
+            job = nj;
+            k = kn;
+            e0 = e0n;
+            cur = nxt;
+        }
+    } else {  // ---- updater: consumers uw and uw + kUpd, alternately
+        // the replica-0 parameters of the chunk it serves next are loaded (into pr) right
+        // after the previous chunk's stores, so they arrive while that consumer transforms
+        const int uw = wid - kCons;
+        __builtin_amdgcn_s_setprio(1);
+        int64_t job[2] = {(int64_t)blockIdx.x * kCons + uw, (int64_t)blockIdx.x * kCons + uw + kUpd};
+        int i_of[2] = {0, 0};
+        int u = 0;
+        if (job[0] >= nchunks) return;
+        ga_demo_tensor td = tens[find_tensor(tens, ntens, -1, (int)job[0])];
+        PRaw<T> pr;
+        dchunk_params<T>(td, (int)job[0] - td.chunk_start, param, ptr_vec, pr);
+        while (true) {
+            const int cw = uw + u * kUpd;
+            const int64_t base = chunk_base(td, (int)job[u] - td.chunk_start);
+            lds_wait_flag(&L.flag[cw], 2 * i_of[u] + 1);
+            apply_signs(reinterpret_cast<const float4*>(L.slot[cw].tile), param + base, grad ? grad + base : nullptr,
+                        K, ld, td.cols, chunk_vec(td, ptr_vec), 64, lr, lane_id(), pr, true);
+            lds_set_flag(&L.flag[cw], 2 * i_of[u] + 2);
+            job[u] += stride;
+            ++i_of[u];
+            // the other consumer's turn, unless its sequence has ended (then this one's)
+            const int nu = job[1 - u] < nchunks ? 1 - u : u;
+            if (job[nu] >= nchunks) break;
+            u = nu;
+            td = tens[find_tensor(tens, ntens, -1, (int)job[u])];
+            dchunk_params<T>(td, (int)job[u] - td.chunk_start, param, ptr_vec, pr);
+        }
+    }
+}
+
+static int dec_lc_enabled() {  // GA_DEMO_DECODE_LC=0: the one-wave-per-chunk kernel for every chunk
+    const char* e = getenv("GA_DEMO_DECODE_LC");
+    return e && e[0] == '0' ? 0 : 1;
+}
+
 template <typename T, int MS>
 static void launch_decode_ms(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks,
                              const ga_demo_rowgroup* groups, int32_t ngroups, const float* F64,
                              const int32_t* payload, int64_t pstride, int64_t M, int S, void* param, void* grad,
                              int64_t K, int64_t ld, float lr, int ptr_vec, hipStream_t stream) {
+    if constexpr (MS == 8) if (nchunks > 0 && dec_lc_enabled()) {  // 64x64 chunks: consumer / updater kernel
+        static const int cus = [] {
+            int dev = 0, n = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+            return n > 0 ? n : 256;
+        }();
+        const int64_t want = ((int64_t)nchunks + kCons - 1) / kCons;
+        const int g = (int)(want < cus ? want : cus);
+        hipLaunchKernelGGL((decode_lc_kernel<T, MS>), dim3(g), dim3(kLcThreads), 0, stream, tens, ntens, nchunks, F64,
+                           payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
+        if (ngroups == 0) return;
+        nchunks = 0;  // the row groups: decode_kernel below
+    }
     auto kern = decode_kernel<T, MS>;
     static const int resident = [&] {
         int per_cu = 0, dev = 0, cus = 0;

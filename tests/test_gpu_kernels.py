@@ -1053,3 +1053,33 @@ def test_demo_encode_loader_consumer_matches_all_in_one(monkeypatch, K, zero_chu
         out[lc] = (host(P), host(D), payload.cpu().numpy())
     for a0, a1, what in zip(out["0"], out["1"], ("p", "delta", "payload")):
         assert np.array_equal(a0, a1), what
+
+
+@pytest.mark.parametrize("S,K,with_grad", [(1, 1, True), (4, 1, False), (8, 3, True)])
+def test_demo_decode_consumer_updater_matches_one_wave(monkeypatch, S, K, with_grad):
+    """ga_demo_decode_sym's consumer/updater kernel (the default for 64x64
+    chunks at S <= 8 sources) against its one-wave-per-chunk kernel
+    (GA_DEMO_DECODE_LC=0): the same per-chunk arithmetic, so params and signs
+    are bit-identical -- S sources with colliding indices, batched replicas,
+    with and without the grad output."""
+    from gym_amd import ops
+    shapes = [(192, 128), (768,), (64, 64), (128, 192), (320,), (64, 256), (1024, 64)]
+    L, plan, a = _demo_setup(shapes, S, seed=40 + S)
+    assert plan.wave_encode
+    P, G, D = t(a["p"]), t(a["g"]), t(a["d"])
+    payload = torch.zeros(S, 2 * plan.M, dtype=torch.int32, device=DEV)
+    ops.demo_encode(plan, P, G, D, payload, 0.01, 0.999, 1.0)  # S sources' payloads
+    if S > 1:  # force collisions: source 1 repeats source 0's indices
+        payload[1, : plan.M] = payload[0, : plan.M]
+    P0 = torch.from_numpy(np.repeat(a["p"][:1], K, axis=0)).to(DEV)
+    out = {}
+    for lc in ("0", "1"):
+        monkeypatch.setenv("GA_DEMO_DECODE_LC", lc)
+        Pk = P0.clone()
+        Gk = torch.zeros_like(Pk) if with_grad else None
+        ops.demo_decode(plan, payload, Pk, Gk, 0.01)
+        out[lc] = (host(Pk), host(Gk) if with_grad else None)
+    assert np.array_equal(out["0"][0], out["1"][0])
+    if with_grad:
+        assert np.array_equal(out["0"][1], out["1"][1])
+        assert np.isin(out["1"][1], (-1.0, 0.0, 1.0)).all()
