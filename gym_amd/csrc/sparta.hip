@@ -22,6 +22,8 @@
 // (one 24-bit draw per element): the mask no longer bounds the kernel.
 #include <math.h>
 
+#include <atomic>
+
 #include "ga_common.h"
 
 namespace ga {
@@ -763,6 +765,167 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
     }
 }
 
+// The same select in ONE pass (no count / scan kernels, the mask drawn once):
+// each workgroup takes the next count tile by an atomic ticket (tickets follow
+// the order workgroups start, so every tile a workgroup waits on is already
+// running), draws its mask, publishes its selected count, and finds its
+// output base by decoupled look-back over the tiles before it (Merrill &
+// Garland): wave 0 reads up to 64 predecessors' status words at once and sums
+// aggregates back to the nearest published inclusive prefix.  A status word
+// is one 8-byte granule {epoch:32, prefix:1, value:31}, written by one lane
+// with a relaxed agent-scope store (sc1) and polled with relaxed agent-scope
+// loads (sc1; MI355X_MICROARCH.md hand-off table, row 1); the per-launch
+// epoch makes earlier launches' words invalid, so the array is never cleared.
+// The last ticket resets the ticket word and writes count[0] / count[1].
+struct LookBack {
+    uint64_t* status;  // [ntiles]
+    uint32_t* ticket;  // zero at launch (the host clears it on the stream)
+    uint32_t epoch;    // nonzero, new per launch
+};
+
+__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, bool prefix, int64_t v) {
+    return ((uint64_t)epoch << 32) | (prefix ? 0x80000000ull : 0ull) | (uint64_t)(v & 0x7fffffff);
+}
+
+// exclusive base of `tile` (whose own count is A) -- called by all 64 lanes of one wave
+__device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_t tile, int64_t A, int lane) {
+    if (tile == 0) {
+        if (lane == 0) __hip_atomic_store(LB.status, lb_word(LB.epoch, true, A), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(LB.status + tile, lb_word(LB.epoch, false, A), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    int64_t excl = 0, j = tile - 1;  // window: tiles j, j - 1, ..., j - 63 on lanes 0..63
+    for (;;) {
+        const int64_t jj = j - lane;
+        uint64_t w = jj >= 0 ? __hip_atomic_load(LB.status + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : lb_word(LB.epoch, true, 0);  // before tile 0: an inclusive prefix of 0
+        const bool valid = (uint32_t)(w >> 32) == LB.epoch;
+        const bool pref = valid && (w & 0x80000000ull);
+        const int64_t v = valid ? (int64_t)(w & 0x7fffffffull) : 0;
+        const uint64_t vm = __ballot(valid), pm = __ballot(pref);
+        // lanes 0 .. m-1 hold valid words (m = first invalid lane)
+        const int m = ~vm ? __builtin_ctzll(~vm) : 64;
+        int take;  // lanes consumed from the window
+        bool done = false;
+        if (pm && __builtin_ctzll(pm) < m) {  // an inclusive prefix, every tile after it valid
+            take = __builtin_ctzll(pm) + 1;
+            done = true;
+        } else {
+            take = m;  // aggregates only
+        }
+        int64_t part = lane < take ? v : 0;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
+        excl += part;
+        if (done) break;
+        j -= take;
+        if (take == 0) __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) __hip_atomic_store(LB.status + tile, lb_word(LB.epoch, true, excl + A), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+template <typename T, int KQ, int SRC>
+__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select1_wave_kernel(
+    Pred P, int64_t n, LookBack LB, int64_t ntiles, const T* __restrict__ src, int64_t ld, int64_t cap,
+    int32_t* __restrict__ idx, T* __restrict__ vals, int64_t* __restrict__ count) {
+    using B = WaveBatchDpp<T, KQ>;
+    __shared__ uint64_t tab[kGapTable];
+    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
+    __shared__ int wave_tot[GA_SP_WAVES];
+    __shared__ int64_t s_tile, s_excl;
+    if (threadIdx.x == 0) {
+        const uint32_t t = atomicAdd(LB.ticket, 1u);
+        if (t == (uint32_t)(ntiles - 1))  // every ticket of this launch is taken: ready for the next one
+            __hip_atomic_store(LB.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_tile = t;
+    }
+    if (SRC != 1) load_gap_table(P, tab);  // (its barrier also publishes s_tile)
+    else __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t tile = s_tile;
+    uint16_t* list = lists[wid];
+    const int64_t tile0 = (tile * GA_SP_WAVES + wid) * kWTile;
+    const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
+    const uint64_t bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
+    const int c = __popcll(bits);
+    int x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    const int total = __shfl(x, 63, 64);
+    const int local0 = x - c;
+    if (lane == 0) wave_tot[wid] = total;
+    __syncthreads();
+    if (wid == 0) {
+        int64_t A = 0;
+#pragma unroll
+        for (int w = 0; w < GA_SP_WAVES; ++w) A += wave_tot[w];
+        const int64_t excl = lookback_exclusive(LB, tile, A, lane);
+        if (lane == 0) {
+            s_excl = excl;
+            if (tile == ntiles - 1) {
+                count[0] = excl + A;
+                count[1] = excl + A > cap ? 1 : 0;
+            }
+        }
+    }
+    __syncthreads();
+    int64_t pos0 = s_excl;
+    for (int w = 0; w < wid; ++w) pos0 += wave_tot[w];
+    {
+        int l = local0;
+        uint64_t b = bits;
+        while (b) {
+            const int j = __builtin_ctzll(b);
+            b &= b - 1;
+            const int64_t pos = pos0 + l;
+            if (pos < cap) idx[pos] = (int32_t)(e0 + j);
+            ++l;
+        }
+    }
+    for (int w0 = 0; w0 < total; w0 += kWList) {  // one window unless p is large
+        {
+            int l = local0;
+            uint64_t b = bits;
+            while (b) {
+                const int j = __builtin_ctzll(b);
+                b &= b - 1;
+                if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * kSpPerThread + j);
+                ++l;
+            }
+        }
+        wave_sync();
+        const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
+        for (int b0 = 0; b0 < wtot; b0 += B::EB)
+            B::sums(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, vals, pos0 + w0, cap);
+    }
+}
+
+template <typename T>
+static bool launch_select1_wave(hipStream_t stream, const Pred& P, int64_t n, const LookBack& LB, const void* src,
+                                int64_t ld, int64_t K, int64_t cap, int32_t* idx, void* vals, int64_t* count) {
+    const int64_t ntiles = ceil_div(n, (int64_t)kSpTile);
+    const dim3 grid((unsigned)ntiles), block(64 * GA_SP_WAVES);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, LB, ntiles, (const T*)src, ld, cap, idx, (T*)vals,
+                           count);
+    };
+    switch (K) {
+        case 4: P.ttab ? go(sparta_select1_wave_kernel<T, 1, 1>) : go(sparta_select1_wave_kernel<T, 1, 2>); return true;
+        case 8: P.ttab ? go(sparta_select1_wave_kernel<T, 2, 1>) : go(sparta_select1_wave_kernel<T, 2, 2>); return true;
+        case 16: P.ttab ? go(sparta_select1_wave_kernel<T, 4, 1>) : go(sparta_select1_wave_kernel<T, 4, 2>); return true;
+        case 32: P.ttab ? go(sparta_select1_wave_kernel<T, 8, 1>) : go(sparta_select1_wave_kernel<T, 8, 2>); return true;
+        case 64: P.ttab ? go(sparta_select1_wave_kernel<T, 16, 1>) : go(sparta_select1_wave_kernel<T, 16, 2>); return true;
+        default: return false;
+    }
+}
+
 template <typename T>
 static bool launch_select_wave(hipStream_t stream, const Pred& P, int64_t n, const int32_t* tile_offsets,
                                const void* src, int64_t ld, int64_t K, int64_t cap, int32_t* idx, void* vals) {
@@ -959,10 +1122,41 @@ static Rep make_rep(int64_t ld, int layout) {
     return R;
 }
 
+// GA_SP_SELECT1=0: the three-pass (count, scan, select) exchange path (A/B)
+static bool select1_enabled() {
+    const char* e = getenv("GA_SP_SELECT1");
+    return !(e && e[0] == '0');
+}
+
+// a new nonzero look-back epoch per launch, process-wide
+static uint32_t next_epoch() {
+    static std::atomic<uint32_t> g{0};
+    uint32_t e;
+    do {
+        e = g.fetch_add(1u, std::memory_order_relaxed) + 1u;
+    } while (e == 0u);
+    return e;
+}
+
 template <typename T>
 static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pred& P, int64_t cap,
                          int32_t* idx, void* vals, int64_t* count, void* work, float divisor, hipStream_t stream) {
     const int64_t ntiles = sparta_tiles(n);
+    const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlotsV4 && R.ei % 4 == 0 &&
+                    ((uintptr_t)src % (4 * sizeof(T))) == 0;
+    if (v4 && idx && vals && count && divisor == 0.f && K >= 4 && K <= 64 && (K & (K - 1)) == 0 &&
+        select1_enabled()) {  // the exchange path's select: one pass, decoupled look-back
+        LookBack LB;
+        LB.status = (uint64_t*)((char*)work + 2 * ntiles * (int64_t)sizeof(int32_t));
+        LB.ticket = (uint32_t*)(LB.status + ntiles);
+        LB.epoch = next_epoch();
+        if (hipMemsetAsync(LB.ticket, 0, sizeof(uint32_t), stream) != hipSuccess) {
+            set_error("ga_sparta_select: ticket reset failed");
+            return GA_EHIP;
+        }
+        if (launch_select1_wave<T>(stream, P, n, LB, src, R.ei, K, cap, idx, vals, count))
+            return check_launch("ga_sparta_select(one pass)");
+    }
     int32_t* tile_offsets = nullptr;
     if (idx || vals || count) {  // positions of the packed list: count + scan passes
         int32_t* tile_counts = (int32_t*)work;
@@ -974,8 +1168,6 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
                            tile_offsets, cap, count);
         if (int e = check_launch("ga_sparta_select(scan)")) return e;
     }
-    const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlotsV4 && R.ei % 4 == 0 &&
-                    ((uintptr_t)src % (4 * sizeof(T))) == 0;
     if (v4 && !tile_offsets && !vals && divisor > 0.f && launch_average_wave<T>(stream, P, n, (void*)src, R.ei, K,
                                                                                 divisor))
         return check_launch("ga_sparta_average_local(wave)");
@@ -998,7 +1190,10 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
 using namespace ga;
 
 extern "C" GA_API int64_t ga_sparta_workspace_bytes(int64_t n) {
-    return 2 * sparta_tiles(n < 0 ? 0 : n) * (int64_t)sizeof(int32_t) + 256;
+    // tile counts + tile offsets (int32 each), the one-pass select's status words (8 B
+    // per tile) and its ticket word
+    const int64_t t = sparta_tiles(n < 0 ? 0 : n);
+    return 2 * t * (int64_t)sizeof(int32_t) + t * (int64_t)sizeof(uint64_t) + 256;
 }
 
 extern "C" GA_API void ga_sparta_gap_table(double p, uint64_t* table) {

@@ -211,7 +211,7 @@ def _mptr(mask):
 
 def sparta_workspace(n, device):
     nbytes = int(lib().ga_sparta_workspace_bytes(int(n)))
-    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+    return torch.zeros(nbytes, dtype=torch.uint8, device=device)  # the one-pass select reads its status words
 
 
 def _sparta_set(t, layout):

@@ -1083,3 +1083,51 @@ def test_demo_decode_consumer_updater_matches_one_wave(monkeypatch, S, K, with_g
     if with_grad:
         assert np.array_equal(out["0"][1], out["1"][1])
         assert np.isin(out["1"][1], (-1.0, 0.0, 1.0)).all()
+
+
+@pytest.mark.parametrize("K,n,p,src_kind", [(32, 1_000_003, 0.005, "philox"), (4, 3 * 16384 + 77, 0.3, "philox"),
+                                            (8, 2_000_000, 0.01, "torch"), (64, 16384 * 5, 0.6, "bits")])
+def test_sparta_one_pass_select_matches_three_pass(monkeypatch, K, n, p, src_kind):
+    """The exchange path's select on an element-major set in ONE pass (ticket
+    + decoupled look-back) against the count -> scan ->
+    select passes (GA_SP_SELECT1=0) and the oracle: the same packed index list,
+    the same K-replica sums, the same count -- launched repeatedly on one
+    workspace (each launch's look-back epoch must ignore the last one's status
+    words), with a cap that overflows on the last launch."""
+    from gym_amd import ops
+    rng = np.random.default_rng(K + n)
+    x = rng.standard_normal((n, K)).astype(np.float32)  # [n, K] element-major
+    src = t(x)
+    seed = 0xABCDEF
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GA_SP_SELECT1", mode)
+        for it in range(3):
+            if src_kind == "philox":
+                m = osparta.philox_mask(n, seed, it, p)
+                kw = dict(seed=seed, iteration=it, p=p)
+            elif src_kind == "bits":
+                m = rng.random(n) < p if mode == "0" else out[("0", it)][3]
+                bits = torch.from_numpy(osparta.pack_mask(m).view(np.int64)).to(DEV)
+                kw = dict(mask=bits)
+            else:  # the in-kernel reference draw (GA_MASK_TORCH)
+                L = __import__("gym_amd.arena", fromlist=["ArenaLayout"]).ArenaLayout([(n,)])
+                table, nb = ops.sparta_bernoulli_table(L.offsets, L.numels, DEV)
+                m = osparta.torch_gpu_bernoulli(n, p, 1234, 12 * it)
+                kw = dict(mask=ops.TorchDraw(table, p, 1234, 12 * it, 12))
+            want = np.flatnonzero(m)
+            cap = len(want) + 16 if it < 2 else max(1, len(want) - 5)  # the last launch overflows
+            idx, count, work = (out[("ws", mode)] if ("ws", mode) in out else _sparta_buffers(n, len(want) + 4096))
+            out[("ws", mode)] = (idx, count, work)
+            vals = torch.empty(cap, device=DEV)
+            ops.sparta_select(src, n, cap, idx, vals, count, work, layout="elem", **kw)
+            c = host(count).astype(np.int64)
+            assert c[0] == len(want) and c[1] == int(len(want) > cap), (mode, it, c, len(want))
+            k = min(cap, len(want))
+            assert np.array_equal(idx.cpu().numpy()[:k], want[:k]), (mode, it)
+            sums = oreduce.mean_reduce(list(x[want[:k]].T), divisor=1)
+            assert np.array_equal(host(vals)[:k], sums), (mode, it)
+            out[(mode, it)] = (idx.cpu().numpy()[:k].copy(), host(vals)[:k].copy(), c, m)
+    for it in range(3):
+        for a, b in zip(out[("0", it)][:3], out[("1", it)][:3]):
+            assert np.array_equal(a, b)
