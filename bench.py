@@ -291,6 +291,7 @@ def bench_diloco(args, coll, dev):
     if coll.world > 1:
         traffic, tnote = None, "not measured at N > 1"
     copy = None if args.pmc_child else stream_copy_rate(dev)
+    args.copy_GBps = copy
     out = {
         "ms_per_step": t * 1e3, "value": value, "K_total": K_total, "n_params": n_params,
         "kernel_ms": kern_ms, "roofline": {
@@ -405,6 +406,24 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
         out["kernel_ms"] = round(kern, 4)
     if conv_ms is not None:
         out["rows_to_elem_transpose_ms"] = round(conv_ms, 3)
+    if layout_kind == "rows" and coll.world == 1 and mask_source == "philox" and "kernel_ms" in out:
+        # what this layout can reach: the same (position, replica) words read and written
+        # back by a bare probe kernel (no mask, no sums) on the positions this step
+        # selected, in this process: the random-word floor.  At the sector granularity
+        # (one 64-B read + one 32-B write sector per word) the copy rate would allow
+        # sector_bytes / copy rate -- random 4-B words do not stream at it.
+        pos = eng.idx[:M]
+        floor_rmw = queued_ms(lambda: ops.probe_random_words(reps, pos, M, write=True), args.steps, dev)
+        floor_rd = queued_ms(lambda: ops.probe_random_words(reps, pos, M, write=False), args.steps, dev)
+        copy = getattr(args, "copy_GBps", None)
+        out["random_word_floor"] = {
+            "probe_rmw_ms": round(floor_rmw, 4), "probe_read_ms": round(floor_rd, 4),
+            "kernel_over_probe_rmw": round(out["kernel_ms"] / floor_rmw, 3),
+            "probe_rmw_sector_GBps": round(sect / (floor_rmw * 1e-3) / 1e9, 1),
+            "sector_floor_ms_at_copy_rate": round(sect / (copy * 1e9) * 1e3, 4) if copy else None,
+            "what": "ga_probe_random_words on this step's selected positions of the same [K, n] set: every "
+                    "(position, replica) fp32 word read and written back (rmw) or read (read), no mask; the rows "
+                    "kernel's floor at this access pattern"}
     return out
 
 

@@ -63,6 +63,42 @@ extern "C" GA_API int ga_stream_copy(const void* src, void* dst, int64_t nbytes,
     return ga::check_launch("ga_stream_copy");
 }
 
+namespace ga {
+
+// Random-word probe: lane f of the grid -> (position j, replica k), replica-major
+// over the whole list (each replica's words of consecutive positions on adjacent
+// lanes), read-modify-write or read + one sum store per 256 lanes.
+__global__ __launch_bounds__(256) void probe_random_words_kernel(float* __restrict__ a, int64_t ld, int64_t K,
+                                                                 const int32_t* __restrict__ pos, int64_t M,
+                                                                 int write) {
+    const int64_t tot = M * K;
+    float acc = 0.f;
+    for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < tot; f += (int64_t)gridDim.x * 256) {
+        const int64_t k = f / M, j = f - k * M;
+        float* p = a + k * ld + pos[j];
+        const float v = *p;
+        if (write) *p = v * 0.5f + 1.f;
+        else acc += v;
+    }
+    if (!write && acc == 12345.678f) a[0] = acc;  // keeps the reads (never true for the probe's data)
+}
+
+}  // namespace ga
+
+extern "C" GA_API int ga_probe_random_words(float* a, int64_t ld, int64_t K, const int32_t* pos, int64_t M,
+                                            int write, hipStream_t stream) {
+    ga::clear_error();
+    GA_REQUIRE(K >= 1 && M >= 0 && ld >= 1, "ga_probe_random_words: bad K/M/ld");
+    if (M == 0) return GA_OK;
+    GA_REQUIRE(a && pos, "ga_probe_random_words: null buffer");
+    const int64_t tot = M * K;
+    int64_t grid = ga::ceil_div(tot, 256);
+    if (grid > 256 * 32) grid = 256 * 32;
+    hipLaunchKernelGGL(ga::probe_random_words_kernel, dim3((unsigned)grid), dim3(256), 0, stream, a, ld, K, pos, M,
+                       write);
+    return ga::check_launch("ga_probe_random_words");
+}
+
 extern "C" GA_API int ga_abi_version(void) { return 103; }
 
 extern "C" GA_API const char* ga_last_error(void) { return ga::g_err; }

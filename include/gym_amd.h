@@ -84,6 +84,18 @@ GA_API const char* ga_last_error(void);
  */
 GA_API int ga_stream_copy(const void* src, void* dst, int64_t nbytes, hipStream_t stream);
 
+/*
+ * Calibration helper (no reference counterpart): the random-word floor of the
+ * [K, ld] rows layout.  For each of the M positions pos[j] (int32, ascending)
+ * and each replica k < K, the fp32 word at a[k * ld + pos[j]] is read and
+ * (write != 0) written back as x * 0.5 + 1, one lane per (position, replica),
+ * replica-major within 16384-element tiles as the SPARTA rows kernel walks
+ * them -- the same 4-B words at random 64-B sectors, without the mask.  bench.py
+ * times it on the positions a SPARTA step selected, in the same process.
+ */
+GA_API int ga_probe_random_words(float* a, int64_t ld, int64_t K, const int32_t* pos, int64_t M, int write,
+                                 hipStream_t stream);
+
 /* ---- mean reduce: SimpleReduce / FedAvg / DiLoCo averaging ------------- */
 
 /*
