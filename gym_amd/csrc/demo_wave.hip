@@ -1215,7 +1215,11 @@ struct DecLDS {
 // float index of (row, col) in the swizzled tile (see t4)
 __device__ __forceinline__ int fidx(int row, int col) { return row * 64 + 4 * ((col >> 2) ^ (row & 15)) + (col & 3); }
 
-__device__ __forceinline__ float sgnf(float g) { return (float)((g > 0.f) - (g < 0.f)); }  // torch.sign, NaN -> 0
+// torch.sign with NaN -> 0: +-1 with g's sign bit where |g| > 0 (false for 0 and NaN), else 0
+// (3 VALU: compare, bit-select, select; the (g > 0) - (g < 0) form issued 6)
+__device__ __forceinline__ float sgnf(float g) {
+    return fabsf(g) > 0.f ? __builtin_copysignf(1.f, g) : 0.f;
+}
 
 // the signs (layout C, read from the tile where used) -> p -= lr * sign, grad = sign,
 // for each of K replicas; a full 64-row chunk's replica 0 comes in pre (loaded before
@@ -1515,10 +1519,15 @@ __device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn<MS>& in, 
                 // the mean over the hitters (demo.py:331-352), applied as the sums are read
                 float4 xv = tile[t4(row, 8 * h + t)];
                 const uint32_t cw = W.aux[(row * 64 + 32 * h + 4 * t) >> 3] >> (16 * (t & 1));
-                xv.x = mean_of(xv.x, cw);
-                xv.y = mean_of(xv.y, cw >> 4);
-                xv.z = mean_of(xv.z, cw >> 8);
-                xv.w = mean_of(xv.w, cw >> 12);
+                // the true divisions only where some lane's four coefficients had two or more
+                // hitters (wave-uniform branch: ~12 VALU per division, 64 per chunk otherwise)
+                const bool multi = ((cw & 0xeu) | ((cw >> 4) & 0xeu) | ((cw >> 8) & 0xeu) | ((cw >> 12) & 0xeu)) != 0u;
+                if (__builtin_amdgcn_ballot_w64(multi)) {
+                    xv.x = mean_of(xv.x, cw);
+                    xv.y = mean_of(xv.y, cw >> 4);
+                    xv.z = mean_of(xv.z, cw >> 8);
+                    xv.w = mean_of(xv.w, cw >> 12);
+                }
                 const float* fr = Hb + l * kLd + 32 * h + 4 * t;
                 ue = mfma(xv.x, fr[0], ue);
                 uo = mfma(xv.y, fr[1], uo);
