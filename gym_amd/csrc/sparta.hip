@@ -702,6 +702,86 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_averag
     }
 }
 
+// Single-process average on the [K, ld] ROWS set (the replica training loop's
+// layout: each node's parameters contiguous), without the packed list.  Every
+// selected (element, replica) is its own random word here, so the step is the
+// latency of ~K x pN scattered reads and writes; the kernel's job is to keep as
+// many of them in flight as the wave slots allow.  One wavefront per 4096-element
+// tile (mask, shuffle scan and LDS list as the element-major wave kernel); then
+// ONE LANE PER LISTED ELEMENT issues all its replicas' loads back to back
+// (up to kRowsKB in flight per lane, 64-bit row offsets), sums them in ascending
+// replica order in the lane (the oracle's sequential fp32 order: bit-identical
+// to the tile-gather kernel), divides, and writes the average to every replica.
+// At p = 0.005 a tile lists ~20 elements: 20 x K words per wave, with no workgroup
+// barrier between the mask draw and the gathers.
+constexpr int kRowsKB = 32;
+template <typename T, int SRC>
+__global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_rows_wave_kernel(Pred P, int64_t n, T* src,
+                                                                                    int64_t ld, int K, float divisor) {
+    __shared__ uint64_t tab[kGapTable];
+    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
+    if (SRC != 1) load_gap_table(P, tab);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint16_t* list = lists[wid];
+    const int64_t tile0 = ((int64_t)blockIdx.x * GA_SP_WAVES + wid) * kWTile;
+    const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
+    const uint64_t bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
+    const int c = __popcll(bits);
+    int x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    const int total = __shfl(x, 63, 64);
+    const int local0 = x - c;
+    for (int w0 = 0; w0 < total; w0 += kWList) {  // one window unless p is large
+        {
+            int l = local0;
+            uint64_t b = bits;
+            while (b) {
+                const int j = __builtin_ctzll(b);
+                b &= b - 1;
+                if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * kSpPerThread + j);
+                ++l;
+            }
+        }
+        wave_sync();
+        const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
+        for (int b0 = 0; b0 < wtot; b0 += 64) {
+            const bool on = b0 + lane < wtot;
+            T* p = src + tile0 + (on ? list[b0 + lane] : 0);
+            float acc = 0.f;
+            for (int k0 = 0; k0 < K; k0 += kRowsKB) {
+                float v[kRowsKB];
+#pragma unroll
+                for (int u = 0; u < kRowsKB; ++u) v[u] = on && k0 + u < K ? Elem<T>::load(p + (int64_t)(k0 + u) * ld) : 0.f;
+#pragma unroll
+                for (int u = 0; u < kRowsKB; ++u)
+                    if (k0 + u < K) acc += v[u];
+            }
+            const float avg = acc / divisor;
+            if (on)
+                for (int k = 0; k < K; ++k) Elem<T>::store(p + (int64_t)k * ld, avg);
+        }
+        wave_sync();  // the list is rewritten by the next window
+    }
+}
+
+template <typename T>
+static bool launch_average_rows_wave(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
+                                     float divisor) {
+    if (K < 1 || K > 4 * kRowsKB) return false;
+    const dim3 grid((unsigned)ceil_div(ceil_div(n, kWTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
+    if (P.ttab)
+        hipLaunchKernelGGL((sparta_average_rows_wave_kernel<T, 1>), grid, block, 0, stream, P, n, (T*)src, ld, (int)K,
+                           divisor);
+    else
+        hipLaunchKernelGGL((sparta_average_rows_wave_kernel<T, 2>), grid, block, 0, stream, P, n, (T*)src, ld, (int)K,
+                           divisor);
+    return true;
+}
+
 // The exchange path's select on the [n, K] layout in the wave form: a
 // workgroup of GA_SP_WAVES wave tiles is exactly one count/scan tile (kSpTile),
 // so its packed-list base comes from tile_offsets and each wave adds the
@@ -1122,6 +1202,12 @@ static Rep make_rep(int64_t ld, int layout) {
     return R;
 }
 
+// GA_SP_ROWS_WAVE=0: the tile-gather kernel for the rows layout's local average (A/B)
+static bool rows_wave_enabled() {
+    const char* e = getenv("GA_SP_ROWS_WAVE");
+    return !(e && e[0] == '0');
+}
+
 // GA_SP_SELECT1=0: the three-pass (count, scan, select) exchange path (A/B)
 static bool select1_enabled() {
     const char* e = getenv("GA_SP_SELECT1");
@@ -1171,6 +1257,9 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
     if (v4 && !tile_offsets && !vals && divisor > 0.f && launch_average_wave<T>(stream, P, n, (void*)src, R.ei, K,
                                                                                 divisor))
         return check_launch("ga_sparta_average_local(wave)");
+    if (!R.em && !tile_offsets && !vals && divisor > 0.f && rows_wave_enabled() &&
+        launch_average_rows_wave<T>(stream, P, n, (void*)src, R.ek, K, divisor))
+        return check_launch("ga_sparta_average_local(rows wave)");
 #ifndef GA_SP_NO_WAVE_SELECT
     if (v4 && tile_offsets && divisor == 0.f &&
         launch_select_wave<T>(stream, P, n, tile_offsets, src, R.ei, K, cap, idx, vals))

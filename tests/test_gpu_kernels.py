@@ -1131,3 +1131,51 @@ def test_sparta_one_pass_select_matches_three_pass(monkeypatch, K, n, p, src_kin
     for it in range(3):
         for a, b in zip(out[("0", it)][:3], out[("1", it)][:3]):
             assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("K,n,p,src_kind,dtype", [(32, 1_000_003, 0.005, "philox", "f32"),
+                                                  (40, 3 * 4096 + 77, 0.3, "philox", "f32"),
+                                                  (5, 200_000, 0.02, "bits", "bf16"),
+                                                  (128, 4096 * 9, 0.9, "bits", "f32"),
+                                                  (8, 2_000_000, 0.01, "torch", "f32"),
+                                                  (1, 70_001, 0.05, "philox", "f32")])
+def test_sparta_rows_wave_matches_tile_gather(monkeypatch, K, n, p, src_kind, dtype):
+    """The replica loop's [K, ld] rows local average in the wave form (one lane
+    per listed element, every replica's word in flight; GA_SP_ROWS_WAVE) against
+    the tile-gather kernel (GA_SP_ROWS_WAVE=0) and the oracle: bit-identical
+    replicas, dense tiles (several list windows, more than 64 elements per
+    batch), K > 32 (several load batches), bf16, each mask source."""
+    from gym_amd import ops
+    rng = np.random.default_rng(K + n)
+    ld = n + 61
+    x = np.zeros((K, ld), np.float32)
+    x[:, :n] = rng.standard_normal((K, n))
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    if src_kind == "philox":
+        m = osparta.philox_mask(n, 0xABC, 5, p)
+        kw = dict(seed=0xABC, iteration=5, p=p)
+    elif src_kind == "bits":
+        m = rng.random(n) < p
+        kw = dict(mask=torch.from_numpy(osparta.pack_mask(m).view(np.int64)).to(DEV))
+    else:
+        L = __import__("gym_amd.arena", fromlist=["ArenaLayout"]).ArenaLayout([(n,)])
+        table, _ = ops.sparta_bernoulli_table(L.offsets, L.numels, DEV)
+        m = osparta.torch_gpu_bernoulli(n, p, 1234, 24)
+        kw = dict(mask=ops.TorchDraw(table, p, 1234, 24, 12))
+    got = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GA_SP_ROWS_WAVE", mode)
+        src = torch.from_numpy(x).to(DEV).to(tdt)
+        ops.sparta_average_local(src, n, float(K), layout="rows", **kw)
+        got[mode] = src.float().cpu().numpy()
+    assert np.array_equal(got["0"], got["1"])
+    if dtype == "f32":
+        want = osparta.sparse_average(list(x[:, :n]), m)
+        for k in range(K):
+            assert np.array_equal(got["1"][k, :n], want[k])
+    else:  # bf16: the fp32 sums of the bf16 inputs, rounded once
+        xb = torch.from_numpy(x).to(tdt).float().numpy()
+        want = osparta.sparse_average(list(xb[:, :n]), m)
+        w = torch.from_numpy(np.stack(want)).to(tdt).float().numpy()
+        assert np.array_equal(got["1"][:, :n], w)
+    assert (got["1"][:, n:] == 0).all()

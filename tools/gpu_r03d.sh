@@ -9,6 +9,18 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_dropin.py -x -v --timeout 120 --timeout-method thread -k "demo or dropin or one_pass or sparta" > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
+for r in 1 2; do
+  for V in 0 1; do
+    line="ROWS_WAVE=$V run $r"
+    for M in sparta_rows sparta_rows_torch; do
+      GA_SP_ROWS_WAVE=$V timeout -k 10 120 python tools/prof_kernels.py $M 20 > $O/${M}_${V}_$r.txt 2>&1 || { echo "$M $V FAILED"; tail -5 $O/${M}_${V}_$r.txt; exit 1; }
+      line="$line $M $(grep '^{' $O/${M}_${V}_$r.txt)"
+    done
+    echo $line
+  done
+done
+timeout -k 10 120 python tools/prof_kernels.py probe_rows 20 > $O/probe_rmw.txt 2>&1 && echo "probe rmw $(cat $O/probe_rmw.txt)" || { echo "PROBE FAILED"; tail -5 $O/probe_rmw.txt; exit 1; }
+GA_PROBE_WRITE=0 timeout -k 10 120 python tools/prof_kernels.py probe_rows 20 > $O/probe_rd.txt 2>&1 && echo "probe read $(cat $O/probe_rd.txt)" || { echo "PROBE FAILED"; tail -5 $O/probe_rd.txt; exit 1; }
 TAG=r03d/ab bash tools/ab_demo_lc.sh || exit 1
 for r in 1 2; do
   for V in 0 1; do

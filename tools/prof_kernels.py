@@ -10,6 +10,8 @@ Modes (BASELINE configs):
   sparta_rows   the same on the [K, n] row layout
   sparta_torch  the same [n, K] step with the reference's torch.bernoulli stream drawn in-kernel (GA_MASK_TORCH)
   torch_draw    ga_sparta_torch_bernoulli: the reference's per-tensor draws for GPT-2 124M as one packed mask
+  sparta_rows_torch  the rows step with the reference draw in-kernel (the replica loop's default at world 1)
+  probe_rows    ga_probe_random_words on fresh p = 0.005 position sets of the rows set (GA_PROBE_WRITE=0: read only)
   diloco        ga_diloco_outer, K=8 GPT-2 124M (configs[2])
 Prints the HIP-event mean per launch and the algorithmic bytes per launch as one JSON line.
 Usage: python tools/prof_kernels.py <mode> [launches]"""
@@ -83,7 +85,7 @@ def main():
             P.copy_(P0)
             alg = 12 * n + 8 * plan.M * S
         out.update(model="gpt2-350m", n=n, M=plan.M)
-    elif mode in ("sparta_torch", "torch_draw"):
+    elif mode in ("sparta_torch", "torch_draw", "sparta_rows_torch"):
         layout = ArenaLayout(MODELS["gpt2-124m"]())
         K, p = 32, 0.005
         table, nblocks = ops.sparta_bernoulli_table(layout.offsets, layout.numels, dev)
@@ -97,16 +99,41 @@ def main():
 
             alg = ops.sparta_mask_words(layout.n) * 8
         else:
-            reps = synth(layout, K, dev).t().contiguous()
+            kind = "rows" if mode == "sparta_rows_torch" else "elem"
+            reps = synth(layout, K, dev)
+            if kind == "elem":
+                reps = reps.t().contiguous()
 
             def step():
                 ops.sparta_average_local(reps, layout.n, float(K), mask=ops.TorchDraw(table, p, 1234, off[0], 12),
-                                         layout="elem")
+                                         layout=kind)
                 off[0] += 12 * len(layout.numels)
 
             alg = 2 * 4 * K * int(round(layout.n * p))
         ms = timed(step, launches)
         out.update(model="gpt2-124m", K=K, p=p, tensors=len(layout.numels))
+    elif mode == "probe_rows":  # the random-word floor of the rows layout (ga_probe_random_words)
+        layout = ArenaLayout(MODELS["gpt2-124m"]())
+        K, p = 32, 0.005
+        reps = synth(layout, K, dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(5)
+        sets = []
+        for _ in range(4):  # a new set of positions per launch (no Infinity-Cache reuse)
+            m = torch.rand(layout.n, device=dev, generator=g) < p
+            sets.append(torch.nonzero(m).reshape(-1).to(torch.int32))
+        it = [0]
+        write = os.environ.get("GA_PROBE_WRITE", "1") == "1"
+
+        def step():
+            pos = sets[it[0] % 4]
+            ops.probe_random_words(reps, pos, pos.numel(), write=write)
+            it[0] += 1
+
+        ms = timed(step, launches)
+        sel = int(sets[0].numel())
+        alg = (2 if write else 1) * 4 * K * sel
+        out.update(model="gpt2-124m", K=K, p=p, write=write, selected=sel)
     elif mode.startswith("sparta"):
         layout = ArenaLayout(MODELS["gpt2-124m"]())
         K, p = 32, 0.005
