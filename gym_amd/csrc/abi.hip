@@ -76,6 +76,18 @@ __global__ __launch_bounds__(256) void probe_random_words_kernel(float* __restri
     for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < tot; f += (int64_t)gridDim.x * 256) {
         const int64_t k = f / M, j = f - k * M;
         float* p = a + k * ld + pos[j];
+        if (write >= 2) {  // the whole aligned 64-B sector (2) or 128-B line (3) read and written back
+            const int nv = write == 2 ? 4 : 8;
+            float4* q = reinterpret_cast<float4*>(a + k * ld + (pos[j] & ~(4 * nv - 1)));
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < nv) v[u] = q[u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < nv) q[u] = make_float4(v[u].x * 0.5f + 1.f, v[u].y, v[u].z, v[u].w);
+            continue;
+        }
         const float v = *p;
         if (write) *p = v * 0.5f + 1.f;
         else acc += v;
@@ -88,7 +100,8 @@ __global__ __launch_bounds__(256) void probe_random_words_kernel(float* __restri
 extern "C" GA_API int ga_probe_random_words(float* a, int64_t ld, int64_t K, const int32_t* pos, int64_t M,
                                             int write, hipStream_t stream) {
     ga::clear_error();
-    GA_REQUIRE(K >= 1 && M >= 0 && ld >= 1, "ga_probe_random_words: bad K/M/ld");
+    GA_REQUIRE(K >= 1 && M >= 0 && ld >= 1 && write >= 0 && write <= 3, "ga_probe_random_words: bad K/M/ld/write");
+    GA_REQUIRE(write < 2 || (ld % 32 == 0 && ((uintptr_t)a % 128) == 0), "ga_probe_random_words: sector modes need 128-B aligned rows");
     if (M == 0) return GA_OK;
     GA_REQUIRE(a && pos, "ga_probe_random_words: null buffer");
     const int64_t tot = M * K;

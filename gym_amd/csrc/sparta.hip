@@ -612,6 +612,33 @@ struct WaveBatchDpp {
             if (q == KQ - 1 && e < ne && pos < cap) Elem<T>::store(vals + pos, a);
         }
     }
+    // the same sums into LDS: out[b0 + e] (the one-pass select writes them after its look-back)
+    __device__ __forceinline__ static void sums_lds(const T* src, int64_t ld, int64_t tile0, const uint16_t* list,
+                                                    int b0, int ne, int lane, float* out) {
+        const int q = lane % KQ, el = lane / KQ;
+        V v[NP];
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int e = u * EPP + el;
+            if (e < ne) v[u] = stream_load(reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q));
+        }
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            if (u * EPP >= ne) break;  // wave-uniform
+            const int e = u * EPP + el;
+            float f[4] = {0.f, 0.f, 0.f, 0.f};
+            if (e < ne) Vec4<T>::unpack(v[u], f);
+            float a = 0.f;
+#pragma unroll
+            for (int s = 0; s < KQ; ++s) {
+                float left = KQ > 1 ? shr1(a) : 0.f;
+                if (q == 0) left = 0.f;
+                const float c = (((left + f[0]) + f[1]) + f[2]) + f[3];
+                a = q == s ? c : a;
+            }
+            if (q == KQ - 1 && e < ne) out[b0 + e] = a;
+        }
+    }
     __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0,
                                                int ne, int lane, float divisor) {
         const int q = lane % KQ, el = lane / KQ;
@@ -848,15 +875,25 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
 // The same select in ONE pass (no count / scan kernels, the mask drawn once):
 // each workgroup takes the next count tile by an atomic ticket (tickets follow
 // the order workgroups start, so every tile a workgroup waits on is already
-// running), draws its mask, publishes its selected count, and finds its
+// running), draws its mask, publishes its selected count at once, gathers its
+// first list window's K-replica sums into LDS, and only then finds its
 // output base by decoupled look-back over the tiles before it (Merrill &
 // Garland): wave 0 reads up to 64 predecessors' status words at once and sums
-// aggregates back to the nearest published inclusive prefix.  A status word
+// aggregates back to the nearest published inclusive prefix; idx and vals are
+// then written coalesced from LDS.  (Looking back BEFORE the gather made every
+// workgroup wait on its predecessors' mask draws: 0.167 ms per forced-exchange
+// step against 0.105 ms for the three passes, profiles/r03d_ab_sparta_select1.txt.)  A status word
 // is one 8-byte granule {epoch:32, prefix:1, value:31}, written by one lane
 // with a relaxed agent-scope store (sc1) and polled with relaxed agent-scope
 // loads (sc1; MI355X_MICROARCH.md hand-off table, row 1); the per-launch
 // epoch makes earlier launches' words invalid, so the array is never cleared.
 // The last ticket resets the ticket word and writes count[0] / count[1].
+// 5 waves per SIMD (96 VGPRs): the one-pass kernel keeps its look-back state
+// beside a gather batch (82 VGPRs); at 8 (64) it spilled 20-84 B per lane, at 6 (80) 12 B
+#ifndef GA_SP1_WPE
+#define GA_SP1_WPE 5
+#endif
+#define GA_SP1_WPE_ATTR __attribute__((amdgpu_waves_per_eu(GA_SP1_WPE, GA_SP1_WPE)))
 struct LookBack {
     uint64_t* status;  // [ntiles]
     uint32_t* ticket;  // zero at launch (the host clears it on the stream)
@@ -867,18 +904,18 @@ __device__ __forceinline__ uint64_t lb_word(uint32_t epoch, bool prefix, int64_t
     return ((uint64_t)epoch << 32) | (prefix ? 0x80000000ull : 0ull) | (uint64_t)(v & 0x7fffffff);
 }
 
-// exclusive base of `tile` (whose own count is A) -- called by all 64 lanes of one wave
+// publish tile's aggregate A (tile 0: its inclusive prefix) -- one lane
+__device__ __forceinline__ void lookback_publish(const LookBack& LB, int64_t tile, int64_t A) {
+    __hip_atomic_store(LB.status + tile, lb_word(LB.epoch, tile == 0, A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exclusive base of `tile` (whose own count is A, already published by
+// lookback_publish) -- called by all 64 lanes of one wave
 __device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_t tile, int64_t A, int lane) {
-    if (tile == 0) {
-        if (lane == 0) __hip_atomic_store(LB.status, lb_word(LB.epoch, true, A), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-        return 0;
-    }
-    if (lane == 0) __hip_atomic_store(LB.status + tile, lb_word(LB.epoch, false, A), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+    if (tile == 0) return 0;
     int64_t excl = 0, j = tile - 1;  // window: tiles j, j - 1, ..., j - 63 on lanes 0..63
     for (;;) {
-        const int64_t jj = j - lane;
+    const int64_t jj = j - lane;
         uint64_t w = jj >= 0 ? __hip_atomic_load(LB.status + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                              : lb_word(LB.epoch, true, 0);  // before tile 0: an inclusive prefix of 0
         const bool valid = (uint32_t)(w >> 32) == LB.epoch;
@@ -909,13 +946,14 @@ __device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_
 }
 
 template <typename T, int KQ, int SRC>
-__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select1_wave_kernel(
+__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP1_WPE_ATTR void sparta_select1_wave_kernel(
     Pred P, int64_t n, LookBack LB, int64_t ntiles, const T* __restrict__ src, int64_t ld, int64_t cap,
     int32_t* __restrict__ idx, T* __restrict__ vals, int64_t* __restrict__ count) {
     using B = WaveBatchDpp<T, KQ>;
     __shared__ uint64_t tab[kGapTable];
     __shared__ uint16_t lists[GA_SP_WAVES][kWList];
     __shared__ int wave_tot[GA_SP_WAVES];
+    __shared__ float sv[GA_SP_WAVES][kWList];
     __shared__ int64_t s_tile, s_excl;
     if (threadIdx.x == 0) {
         const uint32_t t = atomicAdd(LB.ticket, 1u);
@@ -942,34 +980,17 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
     const int local0 = x - c;
     if (lane == 0) wave_tot[wid] = total;
     __syncthreads();
-    if (wid == 0) {
-        int64_t A = 0;
+    int64_t A = 0;
 #pragma unroll
-        for (int w = 0; w < GA_SP_WAVES; ++w) A += wave_tot[w];
-        const int64_t excl = lookback_exclusive(LB, tile, A, lane);
-        if (lane == 0) {
-            s_excl = excl;
-            if (tile == ntiles - 1) {
-                count[0] = excl + A;
-                count[1] = excl + A > cap ? 1 : 0;
-            }
-        }
-    }
-    __syncthreads();
-    int64_t pos0 = s_excl;
-    for (int w = 0; w < wid; ++w) pos0 += wave_tot[w];
-    {
-        int l = local0;
-        uint64_t b = bits;
-        while (b) {
-            const int j = __builtin_ctzll(b);
-            b &= b - 1;
-            const int64_t pos = pos0 + l;
-            if (pos < cap) idx[pos] = (int32_t)(e0 + j);
-            ++l;
-        }
-    }
-    for (int w0 = 0; w0 < total; w0 += kWList) {  // one window unless p is large
+    for (int w = 0; w < GA_SP_WAVES; ++w) A += wave_tot[w];
+    // the tile's aggregate goes out at once, so later tiles' look-backs can pass it
+    // while this tile is still gathering
+    if (threadIdx.x == 0) lookback_publish(LB, tile, A);
+    // window by window (one unless p is large): list + K-replica sums into LDS,
+    // then written out coalesced; the first window is gathered BEFORE the
+    // look-back, so the look-back finds its predecessors resolved
+    int64_t pos0 = 0;
+    for (int w0 = 0;; w0 += kWList) {
         {
             int l = local0;
             uint64_t b = bits;
@@ -981,9 +1002,34 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
             }
         }
         wave_sync();
-        const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
+        const int wtot = total - w0 < kWList ? (total - w0 > 0 ? total - w0 : 0) : kWList;
         for (int b0 = 0; b0 < wtot; b0 += B::EB)
-            B::sums(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, vals, pos0 + w0, cap);
+            B::sums_lds(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, sv[wid]);
+        if (w0 == 0) {  // every wave of the workgroup passes here exactly once
+            if (wid == 0) {
+                const int64_t excl = lookback_exclusive(LB, tile, A, lane);
+                if (lane == 0) {
+                    s_excl = excl;
+                    if (tile == ntiles - 1) {
+                        count[0] = excl + A;
+                        count[1] = excl + A > cap ? 1 : 0;
+                    }
+                }
+            }
+            __syncthreads();
+            pos0 = s_excl;
+            for (int w = 0; w < wid; ++w) pos0 += wave_tot[w];
+        }
+        wave_sync();
+        for (int e = lane; e < wtot; e += 64) {  // consecutive lanes, consecutive list positions
+            const int64_t pos = pos0 + w0 + e;
+            if (pos < cap) {
+                idx[pos] = (int32_t)(tile0 + list[e]);
+                Elem<T>::store(vals + pos, sv[wid][e]);
+            }
+        }
+        if (w0 + kWList >= total) break;
+        wave_sync();  // the list and sums are rewritten by the next window
     }
 }
 

@@ -367,12 +367,14 @@ def stream_copy(src, dst):
 
 def probe_random_words(reps, pos, M, write=True):
     """The random-word floor of a [K, ld] rows set (calibration helper): the
-    fp32 words reps[k, pos[j]] for j < M, read (and written back as x*0.5+1)."""
+    fp32 words reps[k, pos[j]] for j < M, read (and written back as x*0.5+1).
+    write: 0 read, 1 the word read and written back, 2 / 3 the whole aligned
+    64-B sector / 128-B line around it read and written back."""
     _gpu(reps, pos)
     r2 = _as2d(reps)
     if r2.dtype != torch.float32 or pos.dtype != torch.int32 or r2.stride(1) != 1:
         raise ValueError("probe_random_words: fp32 [K, ld] rows, int32 positions")
-    check(lib().ga_probe_random_words(_p(r2), r2.stride(0), r2.shape[0], _p(pos), int(M), int(bool(write)),
+    check(lib().ga_probe_random_words(_p(r2), r2.stride(0), r2.shape[0], _p(pos), int(M), int(write),
                                       _stream()), "ga_probe_random_words")
 
 

@@ -92,6 +92,9 @@ GA_API int ga_stream_copy(const void* src, void* dst, int64_t nbytes, hipStream_
  * replica-major within 16384-element tiles as the SPARTA rows kernel walks
  * them -- the same 4-B words at random 64-B sectors, without the mask.  bench.py
  * times it on the positions a SPARTA step selected, in the same process.
+ * write = 2 / 3: the whole aligned 64-B sector / 128-B line holding the word is
+ * read and written back instead (ld a multiple of 32, a 128-B aligned): what a
+ * full-sector write-back would cost against the word's partial write.
  */
 GA_API int ga_probe_random_words(float* a, int64_t ld, int64_t K, const int32_t* pos, int64_t M, int write,
                                  hipStream_t stream);

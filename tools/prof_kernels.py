@@ -123,7 +123,7 @@ def main():
             m = torch.rand(layout.n, device=dev, generator=g) < p
             sets.append(torch.nonzero(m).reshape(-1).to(torch.int32))
         it = [0]
-        write = os.environ.get("GA_PROBE_WRITE", "1") == "1"
+        write = int(os.environ.get("GA_PROBE_WRITE", "1"))  # 0 read, 1 word rmw, 2 / 3 64-B sector / 128-B line rmw
 
         def step():
             pos = sets[it[0] % 4]
@@ -132,7 +132,7 @@ def main():
 
         ms = timed(step, launches)
         sel = int(sets[0].numel())
-        alg = (2 if write else 1) * 4 * K * sel
+        alg = (2 if write else 1) * 4 * K * sel  # the words' bytes (the sector modes move 16x / 32x)
         out.update(model="gpt2-124m", K=K, p=p, write=write, selected=sel)
     elif mode.startswith("sparta"):
         layout = ArenaLayout(MODELS["gpt2-124m"]())
