@@ -875,18 +875,22 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
 // The same select in ONE pass (no count / scan kernels, the mask drawn once):
 // each workgroup takes the next count tile by an atomic ticket (tickets follow
 // the order workgroups start, so every tile a workgroup waits on is already
-// running), draws its mask, publishes its selected count at once, gathers its
-// first list window's K-replica sums into LDS, and only then finds its
-// output base by decoupled look-back over the tiles before it (Merrill &
-// Garland): wave 0 reads up to 64 predecessors' status words at once and sums
-// aggregates back to the nearest published inclusive prefix; idx and vals are
-// then written coalesced from LDS.  (Looking back BEFORE the gather made every
-// workgroup wait on its predecessors' mask draws: 0.167 ms per forced-exchange
-// step against 0.105 ms for the three passes, profiles/r03d_ab_sparta_select1.txt.)  A status word
-// is one 8-byte granule {epoch:32, prefix:1, value:31}, written by one lane
-// with a relaxed agent-scope store (sc1) and polled with relaxed agent-scope
-// loads (sc1; MI355X_MICROARCH.md hand-off table, row 1); the per-launch
-// epoch makes earlier launches' words invalid, so the array is never cleared.
+// running), draws its mask, publishes its selected count A at once, gathers its
+// first list window's K-replica sums into LDS, and only then computes its
+// output base; idx and vals are then written coalesced from LDS.
+// The base is the sum of the counts of all earlier tiles, kept in two levels
+// so that it never waits on another tile's gather: per tile a status word
+// {epoch:32, count:32} (relaxed agent-scope store; the per-launch epoch makes
+// earlier launches' words invalid, so this array is never cleared) and per
+// SUPER-tile of 64 tiles one 64-bit word {tiles done:32, count sum:32} that
+// each tile bumps with one atomic add of (1 << 32 | A) (zeroed on the stream
+// before the launch).  Wave 0 then reads up to 64 super-tile words and the
+// status words of the earlier tiles of its own super-tile per load, spinning
+// only while an earlier tile has not drawn its mask yet.  (A single-level
+// decoupled look-back either waited on its predecessors' mask draws before the
+// gather -- 0.167 ms per forced-exchange step -- or, after the gather, walked
+// back over thousands of tiles whose inclusive prefixes were not out yet --
+// 0.153 ms; the three passes take 0.108 ms, profiles/r03e_ab_sparta_select1.txt.)
 // The last ticket resets the ticket word and writes count[0] / count[1].
 // 5 waves per SIMD (96 VGPRs): the one-pass kernel keeps its look-back state
 // beside a gather batch (82 VGPRs); at 8 (64) it spilled 20-84 B per lane, at 6 (80) 12 B
@@ -894,55 +898,53 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
 #define GA_SP1_WPE 5
 #endif
 #define GA_SP1_WPE_ATTR __attribute__((amdgpu_waves_per_eu(GA_SP1_WPE, GA_SP1_WPE)))
+constexpr int kSuper = 64;  // tiles per super-tile
 struct LookBack {
-    uint64_t* status;  // [ntiles]
-    uint32_t* ticket;  // zero at launch (the host clears it on the stream)
+    uint64_t* status;  // [ntiles] {epoch, count}
+    uint64_t* super;   // [ceil(ntiles / 64)] {done, sum}, zero at launch
+    uint32_t* ticket;  // zero at launch (the host clears super + ticket on the stream)
     uint32_t epoch;    // nonzero, new per launch
 };
 
-__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, bool prefix, int64_t v) {
-    return ((uint64_t)epoch << 32) | (prefix ? 0x80000000ull : 0ull) | (uint64_t)(v & 0x7fffffff);
-}
-
-// publish tile's aggregate A (tile 0: its inclusive prefix) -- one lane
+// publish tile's count A -- one lane
 __device__ __forceinline__ void lookback_publish(const LookBack& LB, int64_t tile, int64_t A) {
-    __hip_atomic_store(LB.status + tile, lb_word(LB.epoch, tile == 0, A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(LB.status + tile, ((uint64_t)LB.epoch << 32) | (uint64_t)(uint32_t)A, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(LB.super + tile / kSuper, (1ull << 32) | (uint64_t)(uint32_t)A, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// exclusive base of `tile` (whose own count is A, already published by
-// lookback_publish) -- called by all 64 lanes of one wave
-__device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_t tile, int64_t A, int lane) {
-    if (tile == 0) return 0;
-    int64_t excl = 0, j = tile - 1;  // window: tiles j, j - 1, ..., j - 63 on lanes 0..63
-    for (;;) {
-    const int64_t jj = j - lane;
-        uint64_t w = jj >= 0 ? __hip_atomic_load(LB.status + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : lb_word(LB.epoch, true, 0);  // before tile 0: an inclusive prefix of 0
-        const bool valid = (uint32_t)(w >> 32) == LB.epoch;
-        const bool pref = valid && (w & 0x80000000ull);
-        const int64_t v = valid ? (int64_t)(w & 0x7fffffffull) : 0;
-        const uint64_t vm = __ballot(valid), pm = __ballot(pref);
-        // lanes 0 .. m-1 hold valid words (m = first invalid lane)
-        const int m = ~vm ? __builtin_ctzll(~vm) : 64;
-        int take;  // lanes consumed from the window
-        bool done = false;
-        if (pm && __builtin_ctzll(pm) < m) {  // an inclusive prefix, every tile after it valid
-            take = __builtin_ctzll(pm) + 1;
-            done = true;
-        } else {
-            take = m;  // aggregates only
-        }
-        int64_t part = lane < take ? v : 0;
+// exclusive base of `tile` -- called by all 64 lanes of one wave
+__device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_t tile, int lane) {
+    const int64_t S = tile / kSuper, t0 = S * kSuper;
+    int64_t excl = 0;
+    for (int64_t s0 = 0; s0 < S; s0 += 64) {  // whole super-tiles before this one: all 64 tiles counted
+        const int64_t si = s0 + lane;
+        for (;;) {
+            const uint64_t w = si < S ? __hip_atomic_load(LB.super + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : ((uint64_t)kSuper << 32);
+            if (__ballot((w >> 32) != (uint64_t)kSuper) == 0ull) {
+                int64_t part = si < S ? (int64_t)(uint32_t)w : 0;
 #pragma unroll
-        for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
-        excl += part;
-        if (done) break;
-        j -= take;
-        if (take == 0) __builtin_amdgcn_s_sleep(1);
+                for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
+                excl += part;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
     }
-    if (lane == 0) __hip_atomic_store(LB.status + tile, lb_word(LB.epoch, true, excl + A), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
+    const int64_t ti = t0 + lane;  // the earlier tiles of this super-tile
+    for (;;) {
+        const uint64_t w = ti < tile ? __hip_atomic_load(LB.status + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : ((uint64_t)LB.epoch << 32);
+        if (__ballot((uint32_t)(w >> 32) != LB.epoch) == 0ull) {
+            int64_t part = ti < tile ? (int64_t)(uint32_t)w : 0;
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
+            return excl + part;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 template <typename T, int KQ, int SRC>
@@ -1007,7 +1009,7 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP1_WPE_ATTR void sparta_selec
             B::sums_lds(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, sv[wid]);
         if (w0 == 0) {  // every wave of the workgroup passes here exactly once
             if (wid == 0) {
-                const int64_t excl = lookback_exclusive(LB, tile, A, lane);
+                const int64_t excl = lookback_exclusive(LB, tile, lane);
                 if (lane == 0) {
                     s_excl = excl;
                     if (tile == ntiles - 1) {
@@ -1280,9 +1282,11 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
         select1_enabled()) {  // the exchange path's select: one pass, decoupled look-back
         LookBack LB;
         LB.status = (uint64_t*)((char*)work + 2 * ntiles * (int64_t)sizeof(int32_t));
-        LB.ticket = (uint32_t*)(LB.status + ntiles);
+        LB.super = LB.status + ntiles;
+        const int64_t nsuper = ceil_div(ntiles, (int64_t)kSuper);
+        LB.ticket = (uint32_t*)(LB.super + nsuper);
         LB.epoch = next_epoch();
-        if (hipMemsetAsync(LB.ticket, 0, sizeof(uint32_t), stream) != hipSuccess) {
+        if (hipMemsetAsync(LB.super, 0, nsuper * sizeof(uint64_t) + sizeof(uint32_t), stream) != hipSuccess) {
             set_error("ga_sparta_select: ticket reset failed");
             return GA_EHIP;
         }
@@ -1326,9 +1330,10 @@ using namespace ga;
 
 extern "C" GA_API int64_t ga_sparta_workspace_bytes(int64_t n) {
     // tile counts + tile offsets (int32 each), the one-pass select's status words (8 B
-    // per tile) and its ticket word
+    // per tile), super-tile words (8 B per 64 tiles) and its ticket word
     const int64_t t = sparta_tiles(n < 0 ? 0 : n);
-    return 2 * t * (int64_t)sizeof(int32_t) + t * (int64_t)sizeof(uint64_t) + 256;
+    return 2 * t * (int64_t)sizeof(int32_t) + t * (int64_t)sizeof(uint64_t) +
+           ceil_div(t, (int64_t)kSuper) * (int64_t)sizeof(uint64_t) + 256;
 }
 
 extern "C" GA_API void ga_sparta_gap_table(double p, uint64_t* table) {
