@@ -370,7 +370,7 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     kern = timer.mean_ms()
     # events around single launches measure host launch latency at this size; the
     # queued form brackets GPU work only (agrees with rocprofv3's kernel durations)
-    queued = queued_ms(step, args.steps, dev) if coll.world == 1 and mask_source == "philox" else None
+    queued = queued_ms(step, args.steps, dev) if coll.world == 1 else None
     eng.check()
     # the number selected (untimed; the fused single-GPU pass produces no list)
     ops.sparta_select(reps, layout.n, eng.cap, eng.idx, eng.vals, eng.count, eng.work, seed=42, iteration=0, p=p,
@@ -406,12 +406,29 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
         out["kernel_ms"] = round(kern, 4)
     if conv_ms is not None:
         out["rows_to_elem_transpose_ms"] = round(conv_ms, 3)
-    if layout_kind == "rows" and coll.world == 1 and mask_source == "philox" and "kernel_ms" in out:
+    if mask_source == "torch" and coll.world == 1 and "kernel_ms" in out:
+        # the reference draw's VALU roofline: the same n / 4 Philox4x32-10 calls in the
+        # draw's launch shape with nothing compared or stored (ga_probe_philox), and the
+        # draw alone (ga_sparta_torch_bernoulli into the packed words), in this process
+        sink = torch.zeros(1, dtype=torch.int32, device=dev)
+        ceil_ms = queued_ms(lambda: ops.probe_philox(layout.n, sink), args.steps, dev)
+        table, nblocks = ops.sparta_bernoulli_table(layout.offsets, layout.numels, dev)
+        bits = torch.zeros(ops.sparta_mask_words(layout.n), dtype=torch.int64, device=dev)
+        draw_ms = queued_ms(lambda: ops.sparta_torch_bernoulli(table, nblocks, p, 1234, 0, 12, bits), args.steps, dev)
+        out["valu_roofline"] = {
+            "bound": "valu", "philox_calls": -(-layout.n // 4), "philox_ceiling_ms": round(ceil_ms, 4),
+            "draw_alone_ms": round(draw_ms, 4), "draw_frac_of_ceiling": round(ceil_ms / draw_ms, 3),
+            "step_frac_of_ceiling": round(ceil_ms / out["kernel_ms"], 3),
+            "what": "ga_probe_philox: the n/4 Philox4x32-10 calls of the reference's torch.bernoulli stream in the "
+                    "draw's launch shape (one lane per 64-element word, four chains), words XOR-folded, nothing "
+                    "stored -- the arithmetic the reference's stream demands; frac = ceiling / measured"}
+    if layout_kind == "rows" and coll.world == 1 and "kernel_ms" in out:
         # what this layout can reach: the same (position, replica) words read and written
         # back by a bare probe kernel (no mask, no sums) on the positions this step
-        # selected, in this process: the random-word floor.  At the sector granularity
-        # (one 64-B read + one 32-B write sector per word) the copy rate would allow
-        # sector_bytes / copy rate -- random 4-B words do not stream at it.
+        # selected (the Philox draw's: the same number of uniformly random positions as a
+        # reference-draw step), in this process: the random-word floor.  At the sector
+        # granularity (one 64-B read + one 32-B write sector per word) the copy rate would
+        # allow sector_bytes / copy rate -- random 4-B words do not stream at it.
         pos = eng.idx[:M]
         floor_rmw = queued_ms(lambda: ops.probe_random_words(reps, pos, M, write=True), args.steps, dev)
         floor_rd = queued_ms(lambda: ops.probe_random_words(reps, pos, M, write=False), args.steps, dev)
@@ -627,6 +644,8 @@ def main():
     if not args.no_extras and args.only != "diloco":
         runs = [("sparta_k32", bench_sparta),
                 ("sparta_k32_rows", lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows")),
+                ("sparta_k32_rows_torch_mask",  # the replica training loop's own step: rows + the reference draw
+                 lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows", mask_source="torch")),
                 ("sparta_k32_torch_mask", lambda a, c, d: bench_sparta(a, c, d, mask_source="torch")),
                 ("simple_reduce_char_k8", bench_simple),
                 ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]

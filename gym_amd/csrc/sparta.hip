@@ -899,6 +899,9 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
 #endif
 #define GA_SP1_WPE_ATTR __attribute__((amdgpu_waves_per_eu(GA_SP1_WPE, GA_SP1_WPE)))
 constexpr int kSuper = 64;  // tiles per super-tile
+#ifndef GA_SP1_SLEEP
+#define GA_SP1_SLEEP 8  // s_sleep units (64 clocks) between polls of a word not out yet
+#endif
 struct LookBack {
     uint64_t* status;  // [ntiles] {epoch, count}
     uint64_t* super;   // [ceil(ntiles / 64)] {done, sum}, zero at launch
@@ -930,7 +933,7 @@ __device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_
                 excl += part;
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(GA_SP1_SLEEP);
         }
     }
     const int64_t ti = t0 + lane;  // the earlier tiles of this super-tile
@@ -943,7 +946,7 @@ __device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_
             for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
             return excl + part;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(GA_SP1_SLEEP);
     }
 }
 
@@ -1324,6 +1327,32 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
     return check_launch("ga_sparta_select(gather)");
 }
 
+// Calibration (no reference counterpart): the Philox4x32-10 issue ceiling of the
+// reference draw.  One lane per 64-element word runs the 16 calls of torch_word
+// (four independent chains at a time, same counters), XOR-folds the words instead
+// of comparing and packing them and stores nothing: the draw's arithmetic alone.
+__global__ __launch_bounds__(kTbWordLanes) void probe_philox_kernel(int64_t nwords, uint2 key, uint64_t ctr,
+                                                                   uint32_t* sink) {
+    const int64_t wd = (int64_t)blockIdx.x * kTbWordLanes + threadIdx.x;
+    if (wd >= nwords) return;
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int c0 = 0; c0 < 16; c0 += 4) {
+        uint4 w[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint64_t t = (uint64_t)wd * 16 + c0 + c;
+            w[c] = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
+                                 key);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            acc = __builtin_amdgcn_bitop3_b32(acc, __builtin_amdgcn_bitop3_b32(w[c].x, w[c].y, w[c].z, 0x96), w[c].w,
+                                              0x96);
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the calls
+}
+
 }  // namespace ga
 
 using namespace ga;
@@ -1491,6 +1520,16 @@ extern "C" GA_API int ga_sparta_pack_mask(const uint8_t* mask, int64_t n, uint64
 }
 
 extern "C" GA_API int64_t ga_sparta_torch_bernoulli_span(void) { return kTbSpan; }
+
+extern "C" GA_API int ga_probe_philox(int64_t n, uint32_t* sink, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(n >= 0 && sink, "ga_probe_philox: bad n or null sink");
+    const int64_t nwords = ceil_div(n, (int64_t)64);
+    if (nwords == 0) return GA_OK;
+    hipLaunchKernelGGL(probe_philox_kernel, dim3((unsigned)ceil_div(nwords, (int64_t)kTbWordLanes)),
+                       dim3(kTbWordLanes), 0, stream, nwords, make_uint2(0x1234u, 0x5678u), (uint64_t)48, sink);
+    return check_launch("ga_probe_philox");
+}
 
 extern "C" GA_API int ga_sparta_torch_draw_bytes(void) { return (int)sizeof(ga_sparta_torch_draw); }
 

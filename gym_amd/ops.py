@@ -378,6 +378,14 @@ def probe_random_words(reps, pos, M, write=True):
                                       _stream()), "ga_probe_random_words")
 
 
+def probe_philox(n, sink):
+    """The Philox4x32-10 issue ceiling of an n-element reference draw
+    (calibration helper): n / 4 calls in the packed draw's launch shape, no
+    compare, no store.  sink: a uint32/int32 device tensor of >= 1 element."""
+    _gpu(sink)
+    check(lib().ga_probe_philox(int(n), _p(sink), _stream()), "ga_probe_philox")
+
+
 def sumsq_partials(device, K=1):
     return torch.empty(int(K) * int(lib().ga_sumsq_partials_count()), dtype=torch.float32, device=device)
 

@@ -99,6 +99,17 @@ GA_API int ga_stream_copy(const void* src, void* dst, int64_t nbytes, hipStream_
 GA_API int ga_probe_random_words(float* a, int64_t ld, int64_t K, const int32_t* pos, int64_t M, int write,
                                  hipStream_t stream);
 
+/*
+ * Calibration helper (no reference counterpart): the Philox4x32-10 issue
+ * ceiling of the reference's SPARTA mask draw (sparta.py:80-85 through
+ * ga_sparta_torch_bernoulli).  The n / 4 calls an n-element draw makes, in
+ * ga_sparta_torch_bernoulli's packed-word launch shape (one lane per 64
+ * elements, four independent chains), with the words XOR-folded instead of
+ * compared and packed and nothing stored (sink: one device uint32, written only
+ * in the never-taken case).  bench.py times it to give the draw a VALU roofline.
+ */
+GA_API int ga_probe_philox(int64_t n, uint32_t* sink, hipStream_t stream);
+
 /* ---- mean reduce: SimpleReduce / FedAvg / DiLoCo averaging ------------- */
 
 /*

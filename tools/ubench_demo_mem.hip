@@ -56,6 +56,46 @@ __global__ __launch_bounds__(64 * WAVES) void chunk_kernel(float* __restrict__ d
     if (acc[0][5] == 1234.5f) sink[0] = acc[1][3];
 }
 
+// Row-band form: a workgroup of W waves owns a band of W chunks side by side (64 rows x 64 W
+// columns); every load/store instruction covers one contiguous 1-KB row segment (wave w: rows
+// w, w + W, ..., 64 / W rows x W / 4 segments each = 16 instructions per array, as above).
+template <int W>
+__global__ __launch_bounds__(64 * W) void band_kernel(float* __restrict__ delta, const float* __restrict__ grad,
+                                                      int R, int C, long nbands, float* sink) {
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gb = C / (64 * W);  // bands per 64-row strip
+    constexpr int SEG = W / 4;    // 1-KB segments per band row
+    for (long job = blockIdx.x; job < nbands; job += gridDim.x) {
+        const int cy = (int)(job / gb), cx = (int)(job - (long)cy * gb);
+        const long base = (long)cy * 64 * C + (long)cx * 64 * W;
+        float4 D[16], G[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = wid + W * (i / SEG), seg = i % SEG;
+            D[i] = *reinterpret_cast<const float4*>(delta + base + (long)row * C + 256 * seg + 4 * lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = wid + W * (i / SEG), seg = i % SEG;
+            G[i] = *reinterpret_cast<const float4*>(grad + base + (long)row * C + 256 * seg + 4 * lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            D[i].x = fmaf(1e-3f, G[i].x, D[i].x * 0.999f);
+            D[i].y = fmaf(1e-3f, G[i].y, D[i].y * 0.999f);
+            D[i].z = fmaf(1e-3f, G[i].z, D[i].z * 0.999f);
+            D[i].w = fmaf(1e-3f, G[i].w, D[i].w * 0.999f);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = wid + W * (i / SEG), seg = i % SEG;
+            *reinterpret_cast<float4*>(delta + base + (long)row * C + 256 * seg + 4 * lane) = D[i];
+        }
+    }
+    if (lane == 99) sink[0] = 0.f;
+}
+
 __global__ __launch_bounds__(256) void stream3(float4* __restrict__ d, const float4* __restrict__ g, long nv) {
     const long stride = (long)gridDim.x * 256;
     for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < nv; v += stride) {
@@ -95,6 +135,10 @@ int main() {
         RUN(0, 8, 1) RUN(0, 8, 2) RUN(0, 16, 1)
         RUN(128, 8, 1) RUN(128, 8, 2) RUN(128, 16, 1)
         RUN(160, 8, 1) RUN(160, 8, 2)
+#define BAND(W, BPC) { const long nb = (long)(R / 64) * (C / (64 * W)); \
+        float ms = time_ms([&] { band_kernel<W><<<cus * BPC, 64 * W>>>(d, g, R, C, nb, sink); }, 10); \
+        printf("band  C=%d waves/blk=%2d blk/CU=%d          : %.3f ms  %.0f GB/s\n", C, W, BPC, ms, b / ms / 1e6); }
+        BAND(4, 2) BAND(4, 4) BAND(8, 1) BAND(8, 2) BAND(16, 1)
     }
     return 0;
 }
