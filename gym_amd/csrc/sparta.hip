@@ -1259,10 +1259,14 @@ static bool rows_wave_enabled() {
     return !(e && e[0] == '0');
 }
 
-// GA_SP_SELECT1=0: the three-pass (count, scan, select) exchange path (A/B)
+// GA_SP_SELECT1=1: the one-pass select (ticket + two-level look-back) instead of
+// the count, scan and select passes.  Opt-in: every cross-workgroup hand-off in it
+// is a memory-side round trip of several microseconds under the gather's load,
+// and the measured step is 2.7x the three passes' (0.29 vs 0.108 ms,
+// profiles/r03e_ab_sparta_select1.txt)
 static bool select1_enabled() {
     const char* e = getenv("GA_SP_SELECT1");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 // a new nonzero look-back epoch per launch, process-wide
