@@ -1150,11 +1150,14 @@ __global__ __launch_bounds__(kLcThreads) void encode_lc_kernel(
     }
 }
 
-// GA_DEMO_ENCODE_LC=0 selects the all-in-one kernel for the 64x64 chunks too (A/B and
-// parity tests; read at every launch)
+// GA_DEMO_ENCODE_LC=1 selects the loader/consumer kernel for the 64x64 chunks (opt-in:
+// measured 1-4% slower than the all-in-one kernel for the encode and both decodes on
+// one box, profiles/r03d_ab_demo_lc.txt -- the two consumer waves per SIMD that LDS
+// allows are the all-in-one kernel's two waves, and their issue, not the loads, sets
+// the time; read at every launch)
 static int lc_enabled() {
     const char* e = getenv("GA_DEMO_ENCODE_LC");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && e[0] == '1' ? 1 : 0;
 }
 
 template <typename T>
@@ -1772,9 +1775,9 @@ __global__ __launch_bounds__(kLcThreads) void decode_lc_kernel(
     }
 }
 
-static int dec_lc_enabled() {  // GA_DEMO_DECODE_LC=0: the one-wave-per-chunk kernel for every chunk
+static int dec_lc_enabled() {  // GA_DEMO_DECODE_LC=1: the consumer/updater kernel (opt-in, see the encode's)
     const char* e = getenv("GA_DEMO_DECODE_LC");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && e[0] == '1' ? 1 : 0;
 }
 
 template <typename T, int MS>

@@ -1027,8 +1027,8 @@ def test_fused_draw_self_check():
 
 @pytest.mark.parametrize("K,zero_chunks", [(1, False), (3, True)])
 def test_demo_encode_loader_consumer_matches_all_in_one(monkeypatch, K, zero_chunks):
-    """ga_demo_encode_sym's loader/consumer kernel (the default for 64x64
-    chunks) against its all-in-one kernel (GA_DEMO_ENCODE_LC=0): the same
+    """ga_demo_encode_sym's loader/consumer kernel (opt-in, GA_DEMO_ENCODE_LC=1)
+    against its all-in-one kernel (the default, GA_DEMO_ENCODE_LC=0): the same
     arithmetic per chunk, so payload, residual delta and weight-decayed params
     are bit-identical -- over every GPT-2-like chunk kind, batched replicas,
     and all-zero chunks (the > kCand top-k fallback)."""
@@ -1057,9 +1057,9 @@ def test_demo_encode_loader_consumer_matches_all_in_one(monkeypatch, K, zero_chu
 
 @pytest.mark.parametrize("S,K,with_grad", [(1, 1, True), (4, 1, False), (8, 3, True)])
 def test_demo_decode_consumer_updater_matches_one_wave(monkeypatch, S, K, with_grad):
-    """ga_demo_decode_sym's consumer/updater kernel (the default for 64x64
-    chunks at S <= 8 sources) against its one-wave-per-chunk kernel
-    (GA_DEMO_DECODE_LC=0): the same per-chunk arithmetic, so params and signs
+    """ga_demo_decode_sym's consumer/updater kernel (opt-in, GA_DEMO_DECODE_LC=1,
+    64x64 chunks at S <= 8 sources) against its one-wave-per-chunk kernel (the
+    default, GA_DEMO_DECODE_LC=0): the same per-chunk arithmetic, so params and signs
     are bit-identical -- S sources with colliding indices, batched replicas,
     with and without the grad output."""
     from gym_amd import ops
