@@ -13,10 +13,6 @@
 // depend on the launch geometry.  dst may alias src (in-place average): each
 // lane reads every replica of its vector before it writes any, and no two
 // lanes touch the same vector, so the sources carry no __restrict__.
-#include <stdlib.h>
-
-#include <type_traits>
-
 #include "ga_common.h"
 
 namespace ga {
@@ -146,72 +142,6 @@ __global__ __launch_bounds__(kBlock) void diloco_outer_kernel(
     }
 }
 
-// The same step for a compile-time K (8: configs[2]'s nodes per GPU) with the
-// workgroup's vectors software-pipelined: the next vector's K + 2 loads are issued
-// before this vector's stores (different vectors never alias, even in place), so
-// each lane keeps a load set in flight while it writes.  Same arithmetic and
-// order as diloco_outer_kernel (bit-identical); GA_DILOCO_PIPE=0 selects that one.
-template <typename M, int K>
-struct DlSet {
-    float4 r[K];
-    typename Vec4<M>::type m, b;
-};
-
-template <typename M, int K>
-__device__ __forceinline__ void dl_load(DlSet<M, K>& S, const float* src, int64_t ld_src, const M* master,
-                                        const M* mom, bool ld_mom, int64_t v) {
-    using VM = typename Vec4<M>::type;
-#pragma unroll
-    for (int k = 0; k < K; ++k) S.r[k] = stream_load(reinterpret_cast<const float4*>(src + k * ld_src) + v);
-    S.m = stream_load(reinterpret_cast<const VM*>(master) + v);
-    if (ld_mom) S.b = stream_load(reinterpret_cast<const VM*>(mom) + v);
-}
-
-template <typename M, int K>
-__global__ __launch_bounds__(kBlock) void diloco_outer_pipe_kernel(const float* src, int64_t ld_src, int64_t n,
-                                                                   M* master, M* mom, OuterParams op, float* dst,
-                                                                   int64_t K_out, int64_t ld_dst) {
-    using VM = typename Vec4<M>::type;
-    const bool has_mom = op.momentum != 0.f, ld_mom = has_mom && !op.first_step;
-    int64_t lo, hi;
-    chunk_range(n >> 2, lo, hi);
-    int64_t v = lo + threadIdx.x;
-    if (v >= hi) return;
-    DlSet<M, K> S[2];
-    dl_load<M, K>(S[0], src, ld_src, master, mom, ld_mom, v);
-#pragma unroll
-    for (int it = 0; it < (int)(kChunk / kBlock); ++it) {
-        DlSet<M, K>& C = S[it & 1];
-        const int64_t vn = v + kBlock;
-        if (it + 1 < (int)(kChunk / kBlock) && vn < hi) dl_load<M, K>(S[(it + 1) & 1], src, ld_src, master, mom, ld_mom, vn);
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            acc[0] += C.r[k].x;
-            acc[1] += C.r[k].y;
-            acc[2] += C.r[k].z;
-            acc[3] += C.r[k].w;
-        }
-        float m[4], b[4] = {0.f, 0.f, 0.f, 0.f};
-        Vec4<M>::unpack(C.m, m);
-        if (ld_mom) Vec4<M>::unpack(C.b, b);
-        float out[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) out[e] = outer_update(acc[e], m[e], b[e], op);
-        stream_store(reinterpret_cast<VM*>(master) + v, Vec4<M>::pack(m));
-        if (has_mom) stream_store(reinterpret_cast<VM*>(mom) + v, Vec4<M>::pack(b));
-        const float4 o = make_float4(out[0], out[1], out[2], out[3]);
-        for (int64_t j = 0; j < K_out; ++j) stream_store(reinterpret_cast<float4*>(dst + j * ld_dst) + v, o);
-        v = vn;
-        if (v >= hi) break;
-    }
-}
-
-static bool diloco_pipe_enabled() {
-    const char* e = getenv("GA_DILOCO_PIPE");
-    return !(e && e[0] == '0');
-}
-
 static bool aligned(const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; }
 
 template <typename T>
@@ -242,13 +172,6 @@ static int launch_diloco(const void* src, int64_t K, int64_t ld_src, int64_t n, 
     const bool vec = (n % 4 == 0) && (ld_src % 4 == 0) && (ld_dst % 4 == 0) &&
                      aligned(src, vb) && aligned(dst, vb) && aligned(master, vm) &&
                      aligned(mom, vm);
-    if constexpr (std::is_same<T, float>::value) {
-        if (vec && K == 8 && diloco_pipe_enabled()) {
-            hipLaunchKernelGGL((diloco_outer_pipe_kernel<M, 8>), dim3(chunk_grid(n / 4)), dim3(kBlock), 0, stream,
-                               (const float*)src, ld_src, n, (M*)master, (M*)mom, op, (float*)dst, K_out, ld_dst);
-            return check_launch("ga_diloco_outer");
-        }
-    }
     if (vec) {
         hipLaunchKernelGGL((diloco_outer_kernel<T, M, true>), dim3(chunk_grid(n / 4)),
                            dim3(kBlock), 0, stream, (const T*)src, K, ld_src, n, (M*)master,

@@ -1179,32 +1179,3 @@ def test_sparta_rows_wave_matches_tile_gather(monkeypatch, K, n, p, src_kind, dt
         w = torch.from_numpy(np.stack(want)).to(tdt).float().numpy()
         assert np.array_equal(got["1"][:, :n], w)
     assert (got["1"][:, n:] == 0).all()
-
-
-@pytest.mark.parametrize("n,K_out,momentum,first", [(4 * 1024 * 7 + 4 * 300, 8, 0.9, False), (4096 * 4, 1, 0.9, True),
-                                                    (4 * 1024 * 3 + 8, 0, 0.0, False), (1_000_000, 8, 0.9, False)])
-def test_diloco_pipelined_kernel_matches(monkeypatch, n, K_out, momentum, first):
-    """The software-pipelined K = 8 DiLoCo kernel (GA_DILOCO_PIPE, the default for
-    fp32 K = 8) against the one-set-per-iteration kernel (GA_DILOCO_PIPE=0) and the
-    oracle: bit-identical master, momentum and replicas, in place (dst = src),
-    with partial workgroup chunks, without momentum, on the first step."""
-    from gym_amd import ops
-    rng = np.random.default_rng(n)
-    K = 8
-    master = (rng.standard_normal(n) * 0.02).astype(np.float32)
-    reps = (master + rng.standard_normal((K, n)) * 1e-3).astype(np.float32)
-    buf = (rng.standard_normal(n) * 1e-4).astype(np.float32)
-    got = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("GA_DILOCO_PIPE", mode)
-        src, gm, gb = t(reps), t(master), t(buf)
-        ops.diloco_outer(src, gm, gb if momentum else None, src if K_out else None, n, float(K), 0.7, momentum, 0.0,
-                         0.0, momentum > 0, first)
-        got[mode] = (host(src), host(gm), host(gb))
-    for a, b in zip(got["0"], got["1"]):
-        assert np.array_equal(a, b)
-    want_m, _, _ = odiloco.outer_step(master, buf if (momentum and not first) else None, list(reps),
-                                      momentum=momentum, nesterov=momentum > 0)
-    np.testing.assert_allclose(got["1"][1], want_m, rtol=1e-6, atol=1e-9)
-    if K_out:
-        assert (got["1"][0] == got["1"][1][None, :]).all()
