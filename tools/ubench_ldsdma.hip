@@ -70,6 +70,31 @@ __global__ __launch_bounds__(256) void read_glds(const f4* __restrict__ src, f4*
     if (a.x == 1234.5f) dst[0] = a;
 }
 
+// store policies: write-only streams and copies with mixed load/store hints
+template <int ST>  // 0 plain, 1 nt, 2 sc0 sc1 (system scope write-through), 3 sc1
+__device__ __forceinline__ void st(f4* p, f4 v) {
+    if (ST == 0) *p = v;
+    else if (ST == 1) nts(p, v);
+    else if (ST == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+template <int ST>
+__global__ __launch_bounds__(256) void write_only(f4* __restrict__ dst, long nvec) {
+    const long base = (long)blockIdx.x * 1024 + threadIdx.x;
+    const f4 v = {1.f, 2.f, 3.f, (float)threadIdx.x};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st<ST>(dst + base + u * 256, v);
+}
+template <int LDNT, int ST>
+__global__ __launch_bounds__(256) void copy_mix(const f4* __restrict__ src, f4* __restrict__ dst, long nvec) {
+    const long base = (long)blockIdx.x * 1024 + threadIdx.x;
+    f4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = LDNT ? ntl(src + base + u * 256) : src[base + u * 256];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st<ST>(dst + base + u * 256, v[u]);
+}
+
 // DiLoCo K = 8 shape: rows r[0..7] at stride ld, plus master m and momentum b; every
 // vector: sum the 8 rows, update m and b, write m, b and the 8 rows (in place)
 constexpr int K = 8;
@@ -158,6 +183,24 @@ int main() {
         printf("round %d read_reg   %.3f ms %.0f GB/s\n", r, t, 16.0 * nvec / t / 1e6);
         t = time_ms([&] { read_glds<<<grid, 256>>>(a, b, nvec); }, 10);
         printf("round %d read_glds  %.3f ms %.0f GB/s\n", r, t, 16.0 * nvec / t / 1e6);
+        t = time_ms([&] { write_only<0><<<grid, 256>>>(b, nvec); }, 10);
+        printf("round %d write_plain %.3f ms %.0f GB/s\n", r, t, 16.0 * nvec / t / 1e6);
+        t = time_ms([&] { write_only<1><<<grid, 256>>>(b, nvec); }, 10);
+        printf("round %d write_nt    %.3f ms %.0f GB/s\n", r, t, 16.0 * nvec / t / 1e6);
+        t = time_ms([&] { write_only<2><<<grid, 256>>>(b, nvec); }, 10);
+        printf("round %d write_sc01  %.3f ms %.0f GB/s\n", r, t, 16.0 * nvec / t / 1e6);
+        t = time_ms([&] { write_only<3><<<grid, 256>>>(b, nvec); }, 10);
+        printf("round %d write_sc1   %.3f ms %.0f GB/s\n", r, t, 16.0 * nvec / t / 1e6);
+        t = time_ms([&] { copy_mix<0, 0><<<grid, 256>>>(a, b, nvec); }, 10);
+        printf("round %d copy ld- st-   %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
+        t = time_ms([&] { copy_mix<1, 0><<<grid, 256>>>(a, b, nvec); }, 10);
+        printf("round %d copy ldnt st-  %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
+        t = time_ms([&] { copy_mix<0, 1><<<grid, 256>>>(a, b, nvec); }, 10);
+        printf("round %d copy ld- stnt  %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
+        t = time_ms([&] { copy_mix<1, 2><<<grid, 256>>>(a, b, nvec); }, 10);
+        printf("round %d copy ldnt sc01 %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
+        t = time_ms([&] { copy_mix<1, 3><<<grid, 256>>>(a, b, nvec); }, 10);
+        printf("round %d copy ldnt sc1  %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
         t = time_ms([&] { dl_reg<<<(int)(n4 / 1024), 256>>>(reps, ld, mst, mom, n4); }, 10);
         printf("round %d dl_reg     %.3f ms %.0f GB/s\n", r, t, dlb / t / 1e6);
         t = time_ms([&] { dl_glds<<<(int)(n4 / 1024), 256>>>(reps, ld, mst, mom, n4); }, 10);
