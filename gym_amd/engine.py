@@ -252,8 +252,11 @@ class Sparta:
         self.vals = torch.empty(self.cap, dtype=dtype, device=device)
         self.count = torch.zeros(2, dtype=torch.int64, device=device)
         self.work = ops.sparta_workspace(n, device)
-        self._flag_host = torch.zeros(2, dtype=torch.int64, pin_memory=torch.cuda.is_available())
-        self._flag_event = None
+        # overflow flags read back asynchronously: two pinned host slots used in turn, each
+        # with the event of the step that filled it (see check / _poll)
+        self._flag_host = [torch.zeros(2, dtype=torch.int64, pin_memory=torch.cuda.is_available()) for _ in range(2)]
+        self._flag_slot = 0
+        self._pending = []  # [(event, host slot)] of steps not checked yet, oldest first
         self.bits = None  # packed mask broadcast buffer (mask mode with an exchange)
 
     def _ensure_cap(self, cap):
@@ -267,13 +270,23 @@ class Sparta:
 
         The capacity is mean + 16 sigma + 1024 of the Binomial(n, p) count, so
         an overflow has probability < 1e-50 per step; the flag is still read
-        back (asynchronously, no host sync in the step) and raised at the
-        start of the next step, or by an explicit check() -- the strategies
-        call it when training ends, so even the last step is covered."""
-        if self._flag_event is not None:
-            self._flag_event.synchronize()
-            if int(self._flag_host[1]) != 0:
-                raise RuntimeError(f"SPARTA: {int(self._flag_host[0])} elements selected > capacity {self.cap}")
+        back (asynchronously, no host sync in the step) and raised two steps
+        later, or by an explicit check() -- the strategies call it when
+        training ends, so even the last step is covered."""
+        self._poll(0)
+
+    def _poll(self, keep):
+        """Check the oldest pending flags until at most `keep` remain.  A step
+        polls with keep=1: it waits only for the step before the previous one,
+        which the GPU has finished while it ran the previous one, so the host
+        never waits on the GPU mid-stream (with keep=0 every step waited for the
+        previous step's kernels and its own launches ran on an idle GPU)."""
+        while len(self._pending) > keep:
+            ev, hb = self._pending.pop(0)
+            ev.synchronize()
+            if int(hb[1]) != 0:
+                self._pending.clear()
+                raise RuntimeError(f"SPARTA: {int(hb[0])} elements selected > capacity {self.cap}")
 
     def __call__(self, reps, seed=0, iteration=0, mask=None, skip=None, mask_cap=None, mask_shared=False):
         """mask: this process's uint8/bool mask arena (the reference selector's
@@ -318,7 +331,7 @@ class Sparta:
         else:
             if mask is not None:
                 self._ensure_cap(int(mask_cap))
-            self.check()
+            self._poll(1)
             cap_used = self.cap
         if not self.coll.exchange:  # every node is a local replica: one fused pass, no exchange
             ops.sparta_average_local(reps, n, float(self.K_total), mask=mask, seed=seed, iteration=iteration,
@@ -329,12 +342,15 @@ class Sparta:
         self.coll.all_reduce_(self.vals[:cap_used])
         ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps, layout=self.layout)
         if mask is None or mask_cap is not None:  # overflow flag read back asynchronously, checked next step
-            self._flag_host.copy_(self.count, non_blocking=True)
+            hb = self._flag_host[self._flag_slot]
+            self._flag_slot ^= 1
+            hb.copy_(self.count, non_blocking=True)
             if self.device.type == "cuda":
-                self._flag_event = torch.cuda.Event()
-                self._flag_event.record()
-            elif int(self._flag_host[1]) != 0:
-                raise RuntimeError(f"SPARTA: {int(self._flag_host[0])} elements selected > capacity {self.cap}")
+                ev = torch.cuda.Event()
+                ev.record()
+                self._pending.append((ev, hb))
+            elif int(hb[1]) != 0:
+                raise RuntimeError(f"SPARTA: {int(hb[0])} elements selected > capacity {self.cap}")
 
 
 class DeMoCodec:

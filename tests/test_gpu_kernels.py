@@ -1179,3 +1179,45 @@ def test_sparta_rows_wave_matches_tile_gather(monkeypatch, K, n, p, src_kind, dt
         w = torch.from_numpy(np.stack(want)).to(tdt).float().numpy()
         assert np.array_equal(got["1"][:, :n], w)
     assert (got["1"][:, n:] == 0).all()
+
+
+class _LoopColl:
+    """A world-1 'exchange' without a process group (collectives are identities):
+    the Sparta engine takes its multi-rank select -> all-reduce -> scatter path."""
+    world, rank, backend, exchange, rccl = 1, 0, "loop", True, False
+
+    def all_reduce_(self, t, async_op=False):
+        return t
+
+    def broadcast_(self, t, src=0):
+        return t
+
+
+def test_sparta_engine_overflow_raised_two_steps_later():
+    """The exchange path's overflow flag is read back without a host wait in
+    the step: a step polls only the flag of the step before the previous one,
+    so an overflow raises two steps later, and check() raises at once."""
+    from gym_amd.engine import Sparta
+    n, K, p = 100_000, 2, 0.3
+    reps = torch.randn(K, n, device=DEV)
+
+    def small(eng):
+        eng.cap = 8
+        eng.idx = torch.empty(8, dtype=torch.int32, device=DEV)
+        eng.vals = torch.empty(8, device=DEV)
+
+    eng = Sparta(_LoopColl(), K, n, DEV, torch.float32, p)
+    small(eng)
+    eng(reps, seed=1, iteration=0)  # overflows
+    eng(reps, seed=1, iteration=1)  # step 0's flag still pending
+    with pytest.raises(RuntimeError, match="capacity"):
+        eng(reps, seed=1, iteration=2)
+    eng2 = Sparta(_LoopColl(), K, n, DEV, torch.float32, p)
+    small(eng2)
+    eng2(reps, seed=1, iteration=0)
+    with pytest.raises(RuntimeError, match="capacity"):
+        eng2.check()
+    ok = Sparta(_LoopColl(), K, n, DEV, torch.float32, 0.001)
+    for it in range(4):
+        ok(reps, seed=1, iteration=it)
+    ok.check()
