@@ -154,6 +154,45 @@ __global__ __launch_bounds__(256) void dl_glds(f4* __restrict__ reps, long ld, f
     }
 }
 
+// sc1 (device-scope) stores through buffer_store_dwordx4 (__builtin_amdgcn_raw_buffer_store_b128,
+// aux = 16), the workgroup's block as the descriptor base
+__device__ __forceinline__ void st_sc1(f4* base, int idx, f4 v) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, idx * 16, 0, 16);
+}
+__global__ __launch_bounds__(256) void copy_buf_sc1(const f4* __restrict__ src, f4* __restrict__ dst, long nvec) {
+    const long blk = (long)blockIdx.x * 1024;
+    f4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ntl(src + blk + threadIdx.x + u * 256);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st_sc1(dst + blk, threadIdx.x + u * 256, v[u]);
+}
+template <int ST>  // 0 plain, 1 nt, 16 sc1 (buffer store)
+__global__ __launch_bounds__(256) void dl_st(f4* __restrict__ reps, long ld, f4* __restrict__ mst, f4* __restrict__ mom,
+                                             long nvec) {
+    const long lo = (long)blockIdx.x * 1024;
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        const long v = lo + i;
+        f4 r[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) r[k] = ntl(reps + k * ld + v);
+        f4 m = ntl(mst + v), b = ntl(mom + v), o;
+        dl_update(r, m, b, o);
+        if (ST == 16) {
+            st_sc1(mst + lo, i, m);
+            st_sc1(mom + lo, i, b);
+#pragma unroll
+            for (int k = 0; k < K; ++k) st_sc1(reps + k * ld + lo, i, o);
+        } else {
+            st<ST>(mst + v, m);
+            st<ST>(mom + v, b);
+#pragma unroll
+            for (int k = 0; k < K; ++k) st<ST>(reps + k * ld + v, o);
+        }
+    }
+}
+
 template <typename F> float time_ms(F f, int reps) {
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     f(); f(); CK(hipDeviceSynchronize()); CK(hipEventRecord(e0));
@@ -201,6 +240,12 @@ int main() {
         printf("round %d copy ldnt sc01 %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
         t = time_ms([&] { copy_mix<1, 3><<<grid, 256>>>(a, b, nvec); }, 10);
         printf("round %d copy ldnt sc1  %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
+        t = time_ms([&] { copy_buf_sc1<<<grid, 256>>>(a, b, nvec); }, 10);
+        printf("round %d copy ldnt bufsc1 %.3f ms %.0f GB/s\n", r, t, 32.0 * nvec / t / 1e6);
+        t = time_ms([&] { dl_st<0><<<(int)(n4 / 1024), 256>>>(reps, ld, mst, mom, n4); }, 10);
+        printf("round %d dl st plain %.3f ms %.0f GB/s\n", r, t, dlb / t / 1e6);
+        t = time_ms([&] { dl_st<16><<<(int)(n4 / 1024), 256>>>(reps, ld, mst, mom, n4); }, 10);
+        printf("round %d dl st bufsc1 %.3f ms %.0f GB/s\n", r, t, dlb / t / 1e6);
         t = time_ms([&] { dl_reg<<<(int)(n4 / 1024), 256>>>(reps, ld, mst, mom, n4); }, 10);
         printf("round %d dl_reg     %.3f ms %.0f GB/s\n", r, t, dlb / t / 1e6);
         t = time_ms([&] { dl_glds<<<(int)(n4 / 1024), 256>>>(reps, ld, mst, mom, n4); }, 10);
