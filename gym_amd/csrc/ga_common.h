@@ -113,6 +113,25 @@ __device__ __forceinline__ void stream_store(uint2* p, const uint2& v) {
 #endif
 }
 
+// Device-scope (sc1) vector stores for streams written once per launch: the
+// store goes out through buffer_store_dwordx4/x2 ... sc1 with the descriptor based
+// at a WAVE-UNIFORM pointer (a workgroup's block of one row) and the lane's byte
+// offset from it (< 2 GiB).  On MI355X a copy with nt loads and sc1 stores ran
+// 5.91-5.93 TB/s against 5.64-5.68 TB/s with nt stores
+// (tools/ubench_ldsdma.hip, profiles/r03k_ubench_store_policy.txt).
+__device__ __forceinline__ void store_sc1(float4* wg_base, uint32_t idx, const float4& v) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wg_base, 0, 0x7fffffff, 0x00020000);
+    ga_f4 w;
+    w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)(idx * 16u), 0, 16);
+}
+__device__ __forceinline__ void store_sc1(uint2* wg_base, uint32_t idx, const uint2& v) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(wg_base, 0, 0x7fffffff, 0x00020000);
+    ga_u2 w;
+    w.x = v.x; w.y = v.y;
+    __builtin_amdgcn_raw_buffer_store_b64(w, r, (int)(idx * 8u), 0, 16);
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Grid size for a grid-stride streaming kernel: enough workgroups to fill
