@@ -7,7 +7,7 @@ OBJ := $(patsubst gym_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := gym_amd/_lib/libgym_amd.so
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -fvisibility=hidden -Wall -Wno-unused-function
 
-.PHONY: all clean oracle asan
+.PHONY: all clean oracle asan variant
 all: $(LIB)
 
 build/%.o: gym_amd/csrc/%.hip gym_amd/csrc/ga_common.h include/gym_amd.h
@@ -46,3 +46,12 @@ $(ASAN_LIB): $(SRC) gym_amd/csrc/ga_common.h include/gym_amd.h
 	$(HIPCC) $(HIPFLAGS) -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer -shared-libsan \
 		-shared -o $@ $(SRC)
 	@echo "ASan runtime: $(ASAN_RT)"
+
+# A kernel variant of the whole library for same-box A/B (tools/ab_lib.sh loads it
+# through GYM_AMD_LIB): make variant VDEFS="-DGA_DEMO_STORE_SC1=1" VNAME=demosc1
+VNAME ?= variant
+VDEFS ?=
+variant: build/libgym_amd_$(VNAME).so
+build/libgym_amd_$(VNAME).so: $(SRC) gym_amd/csrc/ga_common.h include/gym_amd.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) $(VDEFS) -shared -o $@ $(SRC)

@@ -381,12 +381,25 @@ __device__ __forceinline__ void load_coal(const T* pb, int stride, bool vec, int
     }
 }
 
+// GA_DEMO_STORE_SC1 (a build option, A/B): the chunk's vector stores as device-scope
+// (sc1) buffer stores based at the wave-uniform chunk pointer
+#ifndef GA_DEMO_STORE_SC1
+#define GA_DEMO_STORE_SC1 0
+#endif
+template <typename T>
+__device__ __forceinline__ void store_vec(T* pb, uint32_t off, const typename Vec4<T>::type& v) {
+#if GA_DEMO_STORE_SC1
+    store_sc1(reinterpret_cast<typename Vec4<T>::type*>(pb), off >> 2, v);
+#else
+    *reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, off)) = v;
+#endif
+}
+
 template <typename T>
 __device__ __forceinline__ void store_coal(T* pb, int stride, bool vec, int lane, const float (&o)[16][4]) {
     if (vec) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-            *reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride))) = Vec4<T>::pack(o[i]);
+        for (int i = 0; i < 16; ++i) store_vec(pb, coal_off(i, lane, stride), Vec4<T>::pack(o[i]));
     } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
@@ -1253,7 +1266,7 @@ template <typename T>
 __device__ __forceinline__ void store_quad(T* pb, int i, int stride, bool vec, int lane, const float (&f)[4]) {
     T* a = at_off(pb, coal_off(i, lane, stride));
     if (vec) {
-        *reinterpret_cast<typename Vec4<T>::type*>(a) = Vec4<T>::pack(f);
+        store_vec(pb, coal_off(i, lane, stride), Vec4<T>::pack(f));
     } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) Elem<T>::store(a + e, f[e]);
