@@ -272,62 +272,6 @@ __global__ __launch_bounds__(kSpBlock) void sparta_count_kernel(Pred P, int64_t 
     if (threadIdx.x == 0) tile_counts[blockIdx.x] = total;
 }
 
-// The count pass with the scan folded into its tail: every workgroup publishes
-// its tile count and takes an arrival ticket; the LAST to arrive (all counts are
-// out by then) scans the tile counts into tile offsets, writes count[0] / count[1]
-// and resets the ticket for the next launch -- one launch and one kernel boundary
-// less than count -> scan.  Release: a device-scope fence before the ticket;
-// acquire: one after it in the last workgroup.  `arrivals` must be zero at the
-// first launch (the workspace is allocated zeroed).
-__global__ __launch_bounds__(kSpBlock) void sparta_count_scan_kernel(Pred P, int64_t n, int32_t* tile_counts,
-                                                                    int32_t* tile_offsets, int64_t cap,
-                                                                    int64_t* count, uint32_t* arrivals) {
-    __shared__ int wave_tot[4];
-    __shared__ uint64_t tab[kGapTable];
-    __shared__ uint32_t s_last;
-    load_gap_table(P, tab);
-    const int64_t e0 = (int64_t)blockIdx.x * kSpTile + (int64_t)threadIdx.x * kSpPerThread;
-    const int c = e0 < n ? __popcll(pred_bits64(P, tab, e0, n)) : 0;
-    int total;
-    block_excl_scan_256(c, wave_tot, &total);
-    const uint32_t ntiles = gridDim.x;
-    if (threadIdx.x == 0) {
-        tile_counts[blockIdx.x] = total;
-        __threadfence();
-        s_last = atomicAdd(arrivals, 1u) == ntiles - 1u ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    // the last workgroup: exclusive scan of the ntiles counts, 16 consecutive per lane per pass
-    constexpr int per = 16;
-    int64_t carry = 0;
-    for (uint32_t base = 0; base < ntiles; base += kSpBlock * per) {
-        const uint32_t t0 = base + threadIdx.x * per;
-        int v[per];
-        int sum = 0;
-#pragma unroll
-        for (int i = 0; i < per; ++i) {
-            v[i] = t0 + i < ntiles ? __hip_atomic_load(tile_counts + t0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : 0;
-            sum += v[i];
-        }
-        int pass_tot;
-        int run = block_excl_scan_256(sum, wave_tot, &pass_tot);
-#pragma unroll
-        for (int i = 0; i < per; ++i) {
-            if (t0 + i < ntiles) tile_offsets[t0 + i] = (int32_t)(carry + run);
-            run += v[i];
-        }
-        carry += pass_tot;
-    }
-    if (threadIdx.x == 0) {
-        count[0] = carry;
-        count[1] = carry > cap ? 1 : 0;
-        *arrivals = 0u;
-    }
-}
-
 // One workgroup: exclusive scan of the tile counts -> tile offsets, total and
 // the overflow flag.  The counts are staged through LDS in coalesced passes of
 // kScanChunk tiles (all loads in flight at once), then each lane scans a
@@ -1309,12 +1253,6 @@ static Rep make_rep(int64_t ld, int layout) {
     return R;
 }
 
-// GA_SP_FUSED_SCAN=0: separate count and scan kernels (A/B)
-static bool fused_scan_enabled() {
-    const char* e = getenv("GA_SP_FUSED_SCAN");
-    return !(e && e[0] == '0');
-}
-
 // GA_SP_ROWS_WAVE=0: the tile-gather kernel for the rows layout's local average (A/B)
 static bool rows_wave_enabled() {
     const char* e = getenv("GA_SP_ROWS_WAVE");
@@ -1345,11 +1283,6 @@ template <typename T>
 static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pred& P, int64_t cap,
                          int32_t* idx, void* vals, int64_t* count, void* work, float divisor, hipStream_t stream) {
     const int64_t ntiles = sparta_tiles(n);
-    // workspace: a 256-byte header at a fixed place (word 0: the fused count+scan's
-    // arrival ticket, zero between launches) whatever n the workspace was sized for,
-    // then the per-tile arrays
-    void* hdr = work;
-    if (work) work = (char*)work + 256;
     const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlotsV4 && R.ei % 4 == 0 &&
                     ((uintptr_t)src % (4 * sizeof(T))) == 0;
     if (v4 && idx && vals && count && divisor == 0.f && K >= 4 && K <= 64 && (K & (K - 1)) == 0 &&
@@ -1371,19 +1304,12 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
     if (idx || vals || count) {  // positions of the packed list: count + scan passes
         int32_t* tile_counts = (int32_t*)work;
         tile_offsets = tile_counts + ntiles;
-        if (fused_scan_enabled() && ntiles < (int64_t)UINT32_MAX) {  // count with the scan in its last workgroup
-            uint32_t* arrivals = (uint32_t*)hdr;
-            hipLaunchKernelGGL(sparta_count_scan_kernel, dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
-                               tile_counts, tile_offsets, cap, count, arrivals);
-            if (int e = check_launch("ga_sparta_select(count+scan)")) return e;
-        } else {
-            hipLaunchKernelGGL(sparta_count_kernel, dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
-                               tile_counts);
-            if (int e = check_launch("ga_sparta_select(count)")) return e;
-            hipLaunchKernelGGL(sparta_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream, tile_counts, ntiles,
-                               tile_offsets, cap, count);
-            if (int e = check_launch("ga_sparta_select(scan)")) return e;
-        }
+        hipLaunchKernelGGL(sparta_count_kernel, dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
+                           tile_counts);
+        if (int e = check_launch("ga_sparta_select(count)")) return e;
+        hipLaunchKernelGGL(sparta_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream, tile_counts, ntiles,
+                           tile_offsets, cap, count);
+        if (int e = check_launch("ga_sparta_select(scan)")) return e;
     }
     if (v4 && !tile_offsets && !vals && divisor > 0.f && launch_average_wave<T>(stream, P, n, (void*)src, R.ei, K,
                                                                                 divisor))
@@ -1436,12 +1362,11 @@ __global__ __launch_bounds__(kTbWordLanes) void probe_philox_kernel(int64_t nwor
 using namespace ga;
 
 extern "C" GA_API int64_t ga_sparta_workspace_bytes(int64_t n) {
-    // a 256-byte header (the fused count+scan's arrival ticket), then tile counts + tile
-    // offsets (int32 each), the one-pass select's status words (8 B per tile), super-tile
-    // words (8 B per 64 tiles) and its ticket word (in the last 256 bytes)
+    // tile counts + tile offsets (int32 each), the one-pass select's status words (8 B
+    // per tile), super-tile words (8 B per 64 tiles) and its ticket word
     const int64_t t = sparta_tiles(n < 0 ? 0 : n);
     return 2 * t * (int64_t)sizeof(int32_t) + t * (int64_t)sizeof(uint64_t) +
-           ceil_div(t, (int64_t)kSuper) * (int64_t)sizeof(uint64_t) + 512;
+           ceil_div(t, (int64_t)kSuper) * (int64_t)sizeof(uint64_t) + 256;
 }
 
 extern "C" GA_API void ga_sparta_gap_table(double p, uint64_t* table) {
