@@ -15,7 +15,7 @@
 #include "ga_common.h"
 
 #ifndef GA_ADAM_STORE_SC1
-#define GA_ADAM_STORE_SC1 0
+#define GA_ADAM_STORE_SC1 1
 #endif
 
 namespace ga {

@@ -742,6 +742,7 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_averag
 // At p = 0.005 a tile lists ~20 elements: 20 x K words per wave, with no workgroup
 // barrier between the mask draw and the gathers.
 constexpr int kRowsKB = 32;
+constexpr int kRTile = 64 * kSpPerThread;  // one 64-element group per lane, whatever GA_SP_GROUPS is
 template <typename T, int SRC>
 __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_rows_wave_kernel(Pred P, int64_t n, T* src,
                                                                                     int64_t ld, int K, float divisor) {
@@ -750,7 +751,7 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_rows_wave_ker
     if (SRC != 1) load_gap_table(P, tab);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint16_t* list = lists[wid];
-    const int64_t tile0 = ((int64_t)blockIdx.x * GA_SP_WAVES + wid) * kWTile;
+    const int64_t tile0 = ((int64_t)blockIdx.x * GA_SP_WAVES + wid) * kRTile;
     const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
     const uint64_t bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
     const int c = __popcll(bits);
@@ -799,7 +800,7 @@ template <typename T>
 static bool launch_average_rows_wave(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
                                      float divisor) {
     if (K < 1 || K > 4 * kRowsKB) return false;
-    const dim3 grid((unsigned)ceil_div(ceil_div(n, kWTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
+    const dim3 grid((unsigned)ceil_div(ceil_div(n, kRTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
     if (P.ttab)
         hipLaunchKernelGGL((sparta_average_rows_wave_kernel<T, 1>), grid, block, 0, stream, P, n, (T*)src, ld, (int)K,
                            divisor);

@@ -4,7 +4,7 @@
 # in-tree library (4096-element wave tiles).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-bash tools/gpu_r03o.sh || exit 1
+
 O=gpurun_out/r03p
 mkdir -p $O
 for VN in spg2 spg4; do
