@@ -602,7 +602,9 @@ def main():
     ap.add_argument("--replicas", type=int, default=8, help="simulated nodes per GPU")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--only", default=None, help="diloco|sparta|simple|demo|adamw (profiling runs)")
+    ap.add_argument("--only", default=None,
+                    help="diloco|sparta|simple|demo|adamw or an extras name, e.g. sparta_k32_rows_torch_mask "
+                         "(profiling runs)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -631,9 +633,16 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.backends.cuda.matmul.allow_tf32 = False
 
+    extra_runs = [("sparta_k32", bench_sparta),
+                  ("sparta_k32_rows", lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows")),
+                  ("sparta_k32_rows_torch_mask",  # the replica training loop's own step: rows + the reference draw
+                   lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows", mask_source="torch")),
+                  ("sparta_k32_torch_mask", lambda a, c, d: bench_sparta(a, c, d, mask_source="torch")),
+                  ("simple_reduce_char_k8", bench_simple),
+                  ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
     if args.only and args.only != "diloco":
         fn = {"sparta": bench_sparta, "simple": bench_simple, "demo": bench_demo,
-              "adamw": bench_inner_adamw}[args.only]
+              "adamw": bench_inner_adamw, **dict(extra_runs)}[args.only]
         r = fn(args, coll, dev)
         if coll.rank == 0:
             print(json.dumps({"only": args.only, **r}), flush=True)
@@ -642,13 +651,7 @@ def main():
     head = bench_diloco(args, coll, dev)
     extras = {}
     if not args.no_extras and args.only != "diloco":
-        runs = [("sparta_k32", bench_sparta),
-                ("sparta_k32_rows", lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows")),
-                ("sparta_k32_rows_torch_mask",  # the replica training loop's own step: rows + the reference draw
-                 lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows", mask_source="torch")),
-                ("sparta_k32_torch_mask", lambda a, c, d: bench_sparta(a, c, d, mask_source="torch")),
-                ("simple_reduce_char_k8", bench_simple),
-                ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
+        runs = list(extra_runs)
         if coll.world == 1:
             runs.insert(0, ("diloco_torch_per_tensor_gpu",
                             lambda a, c, d: bench_diloco_torch_gpu(a, c, d, head["ms_per_step"])))
@@ -660,6 +663,8 @@ def main():
                 return r
             runs.insert(0, ("diloco_1_node_per_gpu", diloco_1))
         for name, fn in runs:
+            if coll.rank == 0:  # progress on stderr (the JSON line stays the only stdout line)
+                print(f"[bench] {name}", file=sys.stderr, flush=True)
             torch.cuda.empty_cache()
             t_leg = time.perf_counter()
             try:
