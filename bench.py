@@ -609,6 +609,9 @@ def main():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if os.environ.get("GA_BENCH_WATCHDOG"):  # debugging aid: Python stacks on stderr every N s
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GA_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
     single = args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
     if args.pmc_child:  # a rocprofv3 PMC pass: the headline kernel only, a few launches
         coll = setup_dist(1)
