@@ -64,6 +64,10 @@ def _time_worker(rank, world, port, shapes, threads, steps, warmup, out_path):
     os.dup2(devnull, 1)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    # started from a torchrun-launched bench: the agent's store is not ours (with this
+    # set, rank 0 would not serve the rendezvous and every worker would wait forever)
+    for k in ("TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RUN_ID", "GROUP_RANK", "LOCAL_WORLD_SIZE"):
+        os.environ.pop(k, None)
     torch.set_num_threads(threads)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:

@@ -6,6 +6,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -56,4 +57,16 @@ def test_torch_restatement_matches_reference_golden(tmp_path):
 def test_time_outer_step_runs():
     from oracle.torch_diloco import time_outer_step
     t, threads = time_outer_step([(64, 32), (100,)], nodes=2, cores=2, steps=2, warmup=1)
+    assert t > 0 and threads == 1
+
+
+@pytest.mark.timeout(120)
+def test_cpu_baseline_under_torchrun_env(monkeypatch):
+    """bench.py under torchrun (the forced-exchange rehearsal) times the CPU
+    baseline from a process whose environment names torchrun's agent store
+    (TORCHELASTIC_USE_AGENT_STORE): the baseline's own gloo workers must not
+    use it (they waited forever on a store nobody served)."""
+    from oracle.torch_diloco import time_outer_step
+    monkeypatch.setenv("TORCHELASTIC_USE_AGENT_STORE", "True")
+    t, threads = time_outer_step([(64, 64), (128,)], nodes=2, cores=2, steps=2, warmup=1)
     assert t > 0 and threads == 1
