@@ -729,134 +729,6 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_averag
     }
 }
 
-// The same step as a PERSISTENT wave that overlaps its next tile's mask draw with
-// this tile's gathers: the wave lists tile t, issues the loads of its first batch
-// (NPP passes in flight), then draws tile t + stride's 64-element words -- VALU work
-// (the reference draw: 16 Philox calls per lane) while the loads are out -- and only
-// then sums, averages and writes tile t back.  Waves stop being in lock step (a
-// non-persistent wave draws, then waits on its gathers with the SIMD's VALU idle if
-// its partners are gathering too).  Same per-element sums and order: bit-identical.
-// GA_SP_PIPE=1 selects it (A/B).
-#ifndef GA_SP_PIPE_PASSES
-#define GA_SP_PIPE_PASSES 2
-#endif
-#ifndef GA_SP_PIPE_WPE
-#define GA_SP_PIPE_WPE 6
-#endif
-template <typename T, int KQ, int SRC>
-__global__ __launch_bounds__(64 * GA_SP_WAVES) __attribute__((amdgpu_waves_per_eu(GA_SP_PIPE_WPE, GA_SP_PIPE_WPE)))
-void sparta_average_pipe_kernel(Pred P, int64_t n,
-                                                                                              T* __restrict__ src,
-                                                                                              int64_t ld,
-                                                                                              float divisor) {
-    constexpr int EPP = 64 / KQ, NPP = GA_SP_PIPE_PASSES, EB = NPP * EPP;
-    using V = typename Vec4<T>::type;
-    using B = WaveBatchDpp<T, KQ>;
-    __shared__ uint64_t tab[kGapTable];
-    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
-    if (SRC != 1) load_gap_table(P, tab);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint16_t* list = lists[wid];
-    const int64_t ntile = (n + 64 * kSpPerThread - 1) / (64 * kSpPerThread);
-    const int64_t stride = (int64_t)gridDim.x * GA_SP_WAVES;
-    int64_t t = (int64_t)blockIdx.x * GA_SP_WAVES + wid;
-    uint64_t bits = 0ull;
-    if (t < ntile) {
-        const int64_t e0 = t * (64 * kSpPerThread) + (int64_t)lane * kSpPerThread;
-        bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
-    }
-    const int q = lane % KQ, el = lane / KQ;
-    for (; t < ntile; t += stride) {
-        const int64_t tile0 = t * (64 * kSpPerThread);
-        const int c = __popcll(bits);
-        int x = c;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        const int total = __shfl(x, 63, 64);
-        const int local0 = x - c;
-        const bool one_window = total <= kWList;
-        {
-            int l = local0;
-            uint64_t b = bits;
-            while (b) {
-                const int j = __builtin_ctzll(b);
-                b &= b - 1;
-                if (l < kWList) list[l] = (uint16_t)(lane * kSpPerThread + j);
-                ++l;
-            }
-        }
-        wave_sync();
-        // the first batch's loads go out before the next tile's draw
-        const int ne0 = total < EB ? total : EB;
-        V v[NPP];
-#pragma unroll
-        for (int u = 0; u < NPP; ++u) {
-            const int e = u * EPP + el;
-            if (e < ne0) v[u] = stream_load(reinterpret_cast<const V*>(src + (tile0 + list[e]) * ld + 4 * q));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t bits_t = bits;
-        bits = 0ull;
-        if (t + stride < ntile) {
-            const int64_t e1 = (t + stride) * (64 * kSpPerThread) + (int64_t)lane * kSpPerThread;
-            bits = e1 < n ? pred_bits64<SRC>(P, tab, e1, n) : 0ull;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < NPP; ++u) {
-            if (u * EPP >= ne0) break;  // wave-uniform
-            const int e = u * EPP + el;
-            float f[4] = {0.f, 0.f, 0.f, 0.f};
-            if (e < ne0) Vec4<T>::unpack(v[u], f);
-            float a = 0.f;
-#pragma unroll
-            for (int s2 = 0; s2 < KQ; ++s2) {
-                float left = KQ > 1 ? B::shr1(a) : 0.f;
-                if (q == 0) left = 0.f;
-                const float cc = (((left + f[0]) + f[1]) + f[2]) + f[3];
-                a = q == s2 ? cc : a;
-            }
-            const float avg = __shfl(a / divisor, (lane & ~(KQ - 1)) | (KQ - 1), 64);
-            if (e < ne0) {
-                const float w[4] = {avg, avg, avg, avg};
-                stream_store(reinterpret_cast<V*>(src + (tile0 + list[e]) * ld + 4 * q), Vec4<T>::pack(w));
-            }
-        }
-        if (one_window) {  // the rest of the first window
-            for (int b0 = EB; b0 < total; b0 += B::EB)
-                B::run(src, ld, tile0, list, b0, (total - b0) < B::EB ? (total - b0) : B::EB, lane, divisor);
-        } else {  // p large: every window after the first batch, as the non-persistent kernel does
-            for (int w0 = 0; w0 < total; w0 += kWList) {
-                if (w0 > 0) {
-                    wave_sync();
-                    int l = local0;
-                    uint64_t b = bits_t;
-                    while (b) {
-                        const int j = __builtin_ctzll(b);
-                        b &= b - 1;
-                        if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * kSpPerThread + j);
-                        ++l;
-                    }
-                    wave_sync();
-                }
-                const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
-                for (int b0 = w0 == 0 ? EB : 0; b0 < wtot; b0 += B::EB)
-                    B::run(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, divisor);
-            }
-        }
-        wave_sync();  // the list is rewritten by the next tile
-    }
-}
-
-// GA_SP_PIPE=1: the persistent pipelined form of the element-major local average (A/B)
-static bool pipe_enabled() {
-    const char* e = getenv("GA_SP_PIPE");
-    return e && e[0] == '1';
-}
-
 // Single-process average on the [K, ld] ROWS set (the replica training loop's
 // layout: each node's parameters contiguous), without the packed list.  Every
 // selected (element, replica) is its own random word here, so the step is the
@@ -1204,34 +1076,8 @@ static bool launch_select_wave(hipStream_t stream, const Pred& P, int64_t n, con
 }
 
 template <typename T>
-static bool launch_average_pipe(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
-                                float divisor) {
-    static const int cus = [] {
-        int dev = 0, c = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-        return c > 0 ? c : 256;
-    }();
-    // persistent: GA_SP_WPE waves per SIMD, 4 SIMDs per CU, GA_SP_WAVES waves per workgroup
-    const int64_t ntile = ceil_div(n, (int64_t)(64 * kSpPerThread));
-    int64_t wg = (int64_t)cus * 4 * GA_SP_PIPE_WPE / GA_SP_WAVES;
-    const int64_t need = ceil_div(ntile, (int64_t)GA_SP_WAVES);
-    if (wg > need) wg = need;
-    const dim3 grid((unsigned)wg), block(64 * GA_SP_WAVES);
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, (T*)src, ld, divisor); };
-    if (!P.ttab) return false;  // the reference draw only (the Philox gap draw is cheap: nothing to hide)
-    switch (K) {
-        case 8: go(sparta_average_pipe_kernel<T, 2, 1>); return true;
-        case 16: go(sparta_average_pipe_kernel<T, 4, 1>); return true;
-        case 32: go(sparta_average_pipe_kernel<T, 8, 1>); return true;
-        default: return false;
-    }
-}
-
-template <typename T>
 static bool launch_average_wave(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
                                 float divisor) {
-    if (pipe_enabled() && launch_average_pipe<T>(stream, P, n, src, ld, K, divisor)) return true;
     const dim3 grid((unsigned)ceil_div(ceil_div(n, kWTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, (T*)src, ld, divisor); };
     switch (K) {

@@ -1221,31 +1221,3 @@ def test_sparta_engine_overflow_raised_two_steps_later():
     for it in range(4):
         ok(reps, seed=1, iteration=it)
     ok.check()
-
-
-@pytest.mark.parametrize("K,n,p,dtype", [(32, 2_000_000, 0.005, "f32"), (8, 300_001, 0.3, "f32"),
-                                         (16, 4096 * 37 + 5, 0.9, "bf16"), (32, 70_000, 0.05, "f32")])
-def test_sparta_pipelined_reference_draw_matches(monkeypatch, K, n, p, dtype):
-    """The persistent pipelined element-major local average (GA_SP_PIPE=1: the
-    next tile's reference draw overlaps this tile's gathers) against the
-    wave kernel and the oracle of the reference's torch.bernoulli stream:
-    bit-identical replica sets, dense tiles (several list windows), bf16."""
-    from gym_amd import ops
-    from gym_amd.arena import ArenaLayout
-    rng = np.random.default_rng(K + n)
-    x = rng.standard_normal((n, K)).astype(np.float32)
-    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
-    L = ArenaLayout([(n,)])
-    table, _ = ops.sparta_bernoulli_table(L.offsets, L.numels, DEV)
-    m = osparta.torch_gpu_bernoulli(n, p, 777, 36)
-    got = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("GA_SP_PIPE", mode)
-        src = torch.from_numpy(x).to(DEV).to(tdt)
-        ops.sparta_average_local(src, n, float(K), mask=ops.TorchDraw(table, p, 777, 36, 12), layout="elem")
-        got[mode] = src.float().cpu().numpy()
-    assert np.array_equal(got["0"], got["1"])
-    xb = torch.from_numpy(x).to(tdt).float().numpy()
-    want = np.stack(osparta.sparse_average(list(xb.T), m))
-    want = torch.from_numpy(want).to(tdt).float().numpy()
-    assert np.array_equal(got["1"], want.T)
