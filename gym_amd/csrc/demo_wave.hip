@@ -383,9 +383,6 @@ __device__ __forceinline__ void load_coal(const T* pb, int stride, bool vec, int
 
 // GA_DEMO_STORE_SC1 (a build option, A/B): the chunk's vector stores as device-scope
 // (sc1) buffer stores based at the wave-uniform chunk pointer
-#ifndef GA_DEMO_SKIP_EMPTY
-#define GA_DEMO_SKIP_EMPTY 0
-#endif
 #ifndef GA_DEMO_STORE_SC1
 #define GA_DEMO_STORE_SC1 0
 #endif
@@ -477,9 +474,6 @@ __device__ __forceinline__ void chunk64_tail(const f32x16 (&Y)[2][2], int k, T* 
                 for (int r = 0; r < 16; ++r) {
                     const float v = Y[par][qc][r];
                     const bool cnd = fabsf(v) >= T0c;
-#if GA_DEMO_SKIP_EMPTY  // build option (A/B): registers without a candidate in any lane write nothing
-                    if (__builtin_amdgcn_ballot_w64(cnd) == 0ull) continue;
-#endif
                     L2[cnd ? at : kCand + lane] = make_uint2(posof(par, qc, r), __float_as_uint(v));
                     at += cnd ? 1 : 0;
                 }
