@@ -288,7 +288,10 @@ __device__ __forceinline__ void row_product(const float (&x)[2][8][4], const flo
 // ---- sparse synthesis R = sum_e v_e F[:, b_e] (x) F[:, d_e] in the row-pair layout ----
 // The entries (one per lane where `ent`) as per-parity-of-b lists lstp[par * 64 + i], each
 // padded with a zero entry to whole pairs; np0 / np1 = entry pairs per list.
-constexpr int kSynB = 4;  // entry pairs per synthesis batch (LDS reads issued ahead of the MFMAs)
+#ifndef GA_DEMO_SYNB
+#define GA_DEMO_SYNB 4
+#endif
+constexpr int kSynB = GA_DEMO_SYNB;  // entry pairs per synthesis batch (LDS reads issued ahead of the MFMAs)
 
 __device__ __forceinline__ void parity_lists(uint32_t epos, uint32_t ebits, bool ent, int lane, uint2* lstp,
                                              int& np0, int& np1) {
