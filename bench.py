@@ -501,6 +501,7 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
         pipe_ms = timed_loop(lambda: pipe(P, G, D, 1e-3, 0.999, 0.0), args.steps, args.warmup, coll) * 1e3
         del pipe
     n = numel(shapes)
+    copy = getattr(args, "copy_GBps", None)
     # algorithmic HBM bytes: encode reads delta, g and writes delta (wd = 0) + the
     # payload; decode reads p, writes p and grad + S payloads (8 B per entry)
     enc_bytes = 12 * n + 8 * plan.M
@@ -512,11 +513,18 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
             "encode_HBM_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
             "decode_HBM_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
             "decode_8src_HBM_GBps": round((dec_bytes + 7 * 8 * plan.M) / (dec8_ms * 1e-3) / 1e9, 1),
-            # dense-formulation flops of SURVEY 8(d); the folded kernels issue half of them
-            "encode_dense_TFLOPs": round(2 * flops_one / (enc_ms * 1e-3) / 1e12, 2),
-            "decode_dense_TFLOPs": round(flops_one / (dec_ms * 1e-3) / 1e12, 2),
-            "mfma_f32_peak_TFLOPs": MFMA_F32_TFLOPS, "payload_entries": plan.M,
-            "ref_bytes_tx": plan.reference_bytes()}
+            # against 8 TB/s and against this process's streaming copy (the DiLoCo line's copy_GBps)
+            "encode_frac_hbm": round(enc_bytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "decode_8src_frac_hbm": round((dec_bytes + 7 * 8 * plan.M) / (dec8_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "encode_frac_of_copy": round(enc_bytes / (enc_ms * 1e-3) / 1e9 / copy, 4) if copy else None,
+            "decode_8src_frac_of_copy": (round((dec_bytes + 7 * 8 * plan.M) / (dec8_ms * 1e-3) / 1e9 / copy, 4)
+                                         if copy else None),
+            # the MFMA work the kernels issue: the DCT products folded by F[63-i][k] = (-1)^k F[i][k]
+            # (half the dense formulation's 2 * 64^3 per product) and the residual as sparse synthesis,
+            # so SURVEY 8(d)'s dense flop count is not a bound for them; the MFMA pipe is busy 41% of
+            # the encode's SIMD cycles (profiles/r02l_pmc_demo_encode.txt)
+            "dense_formulation_GFLOP_per_encode": round(2 * flops_one / 1e9, 1),
+            "payload_entries": plan.M, "ref_bytes_tx": plan.reference_bytes()}
 
 
 def bench_diloco_torch_gpu(args, coll, dev, fused_ms, model="gpt2-124m", K=8):
