@@ -1221,3 +1221,29 @@ def test_sparta_engine_overflow_raised_two_steps_later():
     for it in range(4):
         ok(reps, seed=1, iteration=it)
     ok.check()
+
+
+def test_empty_inputs_every_kernel():
+    """n = 0 through every entry point on the device: nothing launched or an
+    empty launch, no error, counts written as zero, buffers untouched."""
+    from gym_amd import ops
+    K = 3
+    reps = torch.full((K, 64), 5.0, device=DEV)
+    master, mom = torch.full((64,), 2.0, device=DEV), torch.zeros(64, device=DEV)
+    ops.replica_mean(reps, reps, n=0)
+    ops.diloco_outer(reps, master, mom, reps, 0, float(K), 0.7, 0.9, 0.0, 0.0, True, True)
+    cap = 16
+    idx = torch.full((cap,), -1, dtype=torch.int32, device=DEV)
+    vals = torch.full((cap,), 9.0, device=DEV)
+    count = torch.full((2,), 7, dtype=torch.int64, device=DEV)
+    work = ops.sparta_workspace(1, DEV)
+    ops.sparta_select(reps, 0, cap, idx, vals, count, work, seed=1, iteration=0, p=0.5)
+    assert host(count).tolist() == [0, 0]
+    ops.sparta_scatter(vals, idx, count, cap, float(K), reps)
+    ops.sparta_average_local(reps, 0, float(K), seed=1, iteration=0, p=0.5)
+    g = torch.zeros_like(reps)
+    ops.adam_step(reps, g, torch.zeros_like(reps), torch.zeros_like(reps), 0.1, 0.999, 0.001, 1e-8, 1.0, 0.0,
+                  -1e-3, 1.0, n=0)
+    torch.cuda.synchronize()
+    assert (host(reps) == 5.0).all() and (host(master) == 2.0).all() and (host(vals) == 9.0).all()
+    assert (host(idx) == -1).all()
