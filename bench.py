@@ -391,6 +391,7 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
                    f"select+gather, {'RCCL' if coll.rccl else coll.backend} all-reduce of packed values, scatter",
            "mask_source": mask_source}
     if mask_source == "torch":
+        out["mask_draw"] = draw.mode  # "fused" (ga_sparta_torch_bernoulli) or "torch" (the per-tensor fallback)
         out["mask"] = ("the reference's per-tensor torch.bernoulli draws, bit-identical, " +
                        ("drawn inside the average kernel (GA_MASK_TORCH), in the step" if coll.world == 1 and
                         not coll.exchange else "as one ga_sparta_torch_bernoulli launch writing the packed mask, "
