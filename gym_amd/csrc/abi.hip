@@ -112,6 +112,75 @@ extern "C" GA_API int ga_probe_random_words(float* a, int64_t ld, int64_t K, con
     return ga::check_launch("ga_probe_random_words");
 }
 
+namespace ga {
+
+// The DeMo codec's 64x64-chunk access pattern with no transform: one wavefront per
+// chunk of a [rows, cols] fp32 matrix (persistent over the grid, 8 waves per
+// workgroup, the chunk kernels' coalesced layout -- lane t holds rows (t >> 4) + 4i,
+// i < 16, at column 4 (t & 15)).  mode 0 = the encode's traffic (read a and b,
+// a <- 0.999 a + 1e-3 b), mode 1 = the decode's (read a, write a and b).
+__global__ __launch_bounds__(512) void probe_chunk_stream_kernel(float* __restrict__ a, float* __restrict__ b,
+                                                                 int64_t rows, int64_t cols, int mode) {
+    const int lane = threadIdx.x & 63;
+    const int64_t gx = cols / 64, nch = (rows / 64) * gx;
+    for (int64_t c = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6); c < nch; c += (int64_t)gridDim.x * 8) {
+        const int64_t cy = c / gx, cx = c - cy * gx;
+        float* pa = a + cy * 64 * cols + cx * 64;
+        float* pb = b + cy * 64 * cols + cx * 64;
+        float4 x[16], y[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(pa + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15));
+        if (mode == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) y[i] = *reinterpret_cast<const float4*>(pb + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15));
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                x[i].x = fmaf(1e-3f, y[i].x, 0.999f * x[i].x);
+                x[i].y = fmaf(1e-3f, y[i].y, 0.999f * x[i].y);
+                x[i].z = fmaf(1e-3f, y[i].z, 0.999f * x[i].z);
+                x[i].w = fmaf(1e-3f, y[i].w, 0.999f * x[i].w);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                y[i] = make_float4(x[i].x > 0.f ? 1.f : -1.f, x[i].y > 0.f ? 1.f : -1.f, x[i].z > 0.f ? 1.f : -1.f,
+                                   x[i].w > 0.f ? 1.f : -1.f);
+                x[i].x -= 1e-3f * y[i].x;
+                x[i].y -= 1e-3f * y[i].y;
+                x[i].z -= 1e-3f * y[i].z;
+                x[i].w -= 1e-3f * y[i].w;
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) *reinterpret_cast<float4*>(pb + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15)) = y[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) *reinterpret_cast<float4*>(pa + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15)) = x[i];
+    }
+}
+
+}  // namespace ga
+
+extern "C" GA_API int ga_probe_chunk_stream(float* a, float* b, int64_t rows, int64_t cols, int mode,
+                                            hipStream_t stream) {
+    ga::clear_error();
+    GA_REQUIRE(rows >= 0 && cols >= 0 && rows % 64 == 0 && cols % 64 == 0 && (mode == 0 || mode == 1),
+               "ga_probe_chunk_stream: rows, cols multiples of 64, mode 0 or 1");
+    if (rows == 0 || cols == 0) return GA_OK;
+    GA_REQUIRE(a && b && ((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0, "ga_probe_chunk_stream: buffers");
+    static const int cus = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return c > 0 ? c : 256;
+    }();
+    const int64_t nch = (rows / 64) * (cols / 64);
+    int64_t grid = ga::ceil_div(nch, 8);
+    if (grid > cus) grid = cus;  // one 8-wave workgroup per CU, persistent (as ga_demo_encode_sym)
+    hipLaunchKernelGGL(ga::probe_chunk_stream_kernel, dim3((unsigned)grid), dim3(512), 0, stream, a, b, rows, cols,
+                       mode);
+    return ga::check_launch("ga_probe_chunk_stream");
+}
+
 extern "C" GA_API int ga_abi_version(void) { return 103; }
 
 extern "C" GA_API const char* ga_last_error(void) { return ga::g_err; }

@@ -386,6 +386,17 @@ def probe_philox(n, sink):
     check(lib().ga_probe_philox(int(n), _p(sink), _stream()), "ga_probe_philox")
 
 
+def probe_chunk_stream(a, b, rows, cols, mode):
+    """The DeMo codec's 64x64-chunk memory floor (calibration helper): a, b fp32
+    buffers of >= rows * cols elements viewed as [rows, cols]; mode 0 = the
+    encode's traffic, 1 = the decode's (include/gym_amd.h)."""
+    _gpu(a, b)
+    if a.dtype != torch.float32 or b.dtype != torch.float32 or min(a.numel(), b.numel()) < rows * cols:
+        raise ValueError("probe_chunk_stream: fp32 buffers of rows * cols elements")
+    check(lib().ga_probe_chunk_stream(_p(a), _p(b), int(rows), int(cols), int(mode), _stream()),
+          "ga_probe_chunk_stream")
+
+
 def sumsq_partials(device, K=1):
     return torch.empty(int(K) * int(lib().ga_sumsq_partials_count()), dtype=torch.float32, device=device)
 

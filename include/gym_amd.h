@@ -110,6 +110,17 @@ GA_API int ga_probe_random_words(float* a, int64_t ld, int64_t K, const int32_t*
  */
 GA_API int ga_probe_philox(int64_t n, uint32_t* sink, hipStream_t stream);
 
+/*
+ * Calibration helper (no reference counterpart): the memory floor of the DeMo
+ * codec's access pattern (demo_impl/demo.py:142-209 through ga_demo_encode_sym /
+ * ga_demo_decode_sym).  One wavefront per 64x64 chunk of a [rows, cols] fp32
+ * matrix (rows, cols multiples of 64), the chunk kernels' grid and coalesced
+ * layout, no transform: mode 0 reads a and b and writes a (the encode's 12 B per
+ * element), mode 1 reads a and writes a and b (the decode's).  bench.py prices
+ * the codec kernels against it on a matrix of the model's size.
+ */
+GA_API int ga_probe_chunk_stream(float* a, float* b, int64_t rows, int64_t cols, int mode, hipStream_t stream);
+
 /* ---- mean reduce: SimpleReduce / FedAvg / DiLoCo averaging ------------- */
 
 /*
