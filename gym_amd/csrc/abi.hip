@@ -119,6 +119,18 @@ namespace ga {
 // workgroup, the chunk kernels' coalesced layout -- lane t holds rows (t >> 4) + 4i,
 // i < 16, at column 4 (t & 15)).  mode 0 = the encode's traffic (read a and b,
 // a <- 0.999 a + 1e-3 b), mode 1 = the decode's (read a, write a and b).
+template <bool NT>
+__device__ __forceinline__ float4 pld(const float* p) {
+    if constexpr (NT) return stream_load(reinterpret_cast<const float4*>(p));
+    else return *reinterpret_cast<const float4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void pst(float* p, const float4& v) {
+    if constexpr (NT) stream_store(reinterpret_cast<float4*>(p), v);
+    else *reinterpret_cast<float4*>(p) = v;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(512) void probe_chunk_stream_kernel(float* __restrict__ a, float* __restrict__ b,
                                                                  int64_t rows, int64_t cols, int mode) {
     const int lane = threadIdx.x & 63;
@@ -129,10 +141,10 @@ __global__ __launch_bounds__(512) void probe_chunk_stream_kernel(float* __restri
         float* pb = b + cy * 64 * cols + cx * 64;
         float4 x[16], y[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(pa + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15));
+        for (int i = 0; i < 16; ++i) x[i] = pld<NT>(pa + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15));
         if (mode == 0) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) y[i] = *reinterpret_cast<const float4*>(pb + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15));
+            for (int i = 0; i < 16; ++i) y[i] = pld<NT>(pb + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15));
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 x[i].x = fmaf(1e-3f, y[i].x, 0.999f * x[i].x);
@@ -151,10 +163,10 @@ __global__ __launch_bounds__(512) void probe_chunk_stream_kernel(float* __restri
                 x[i].w -= 1e-3f * y[i].w;
             }
 #pragma unroll
-            for (int i = 0; i < 16; ++i) *reinterpret_cast<float4*>(pb + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15)) = y[i];
+            for (int i = 0; i < 16; ++i) pst<NT>(pb + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15), y[i]);
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) *reinterpret_cast<float4*>(pa + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15)) = x[i];
+        for (int i = 0; i < 16; ++i) pst<NT>(pa + ((lane >> 4) + 4 * i) * cols + 4 * (lane & 15), x[i]);
     }
 }
 
@@ -163,8 +175,8 @@ __global__ __launch_bounds__(512) void probe_chunk_stream_kernel(float* __restri
 extern "C" GA_API int ga_probe_chunk_stream(float* a, float* b, int64_t rows, int64_t cols, int mode,
                                             hipStream_t stream) {
     ga::clear_error();
-    GA_REQUIRE(rows >= 0 && cols >= 0 && rows % 64 == 0 && cols % 64 == 0 && (mode == 0 || mode == 1),
-               "ga_probe_chunk_stream: rows, cols multiples of 64, mode 0 or 1");
+    GA_REQUIRE(rows >= 0 && cols >= 0 && rows % 64 == 0 && cols % 64 == 0 && mode >= 0 && mode <= 3,
+               "ga_probe_chunk_stream: rows, cols multiples of 64, mode 0..3");
     if (rows == 0 || cols == 0) return GA_OK;
     GA_REQUIRE(a && b && ((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0, "ga_probe_chunk_stream: buffers");
     static const int cus = [] {
@@ -176,8 +188,12 @@ extern "C" GA_API int ga_probe_chunk_stream(float* a, float* b, int64_t rows, in
     const int64_t nch = (rows / 64) * (cols / 64);
     int64_t grid = ga::ceil_div(nch, 8);
     if (grid > cus) grid = cus;  // one 8-wave workgroup per CU, persistent (as ga_demo_encode_sym)
-    hipLaunchKernelGGL(ga::probe_chunk_stream_kernel, dim3((unsigned)grid), dim3(512), 0, stream, a, b, rows, cols,
-                       mode);
+    if (mode & 2)
+        hipLaunchKernelGGL(ga::probe_chunk_stream_kernel<true>, dim3((unsigned)grid), dim3(512), 0, stream, a, b,
+                           rows, cols, mode & 1);
+    else
+        hipLaunchKernelGGL(ga::probe_chunk_stream_kernel<false>, dim3((unsigned)grid), dim3(512), 0, stream, a, b,
+                           rows, cols, mode & 1);
     return ga::check_launch("ga_probe_chunk_stream");
 }
 

@@ -389,7 +389,7 @@ def probe_philox(n, sink):
 def probe_chunk_stream(a, b, rows, cols, mode):
     """The DeMo codec's 64x64-chunk memory floor (calibration helper): a, b fp32
     buffers of >= rows * cols elements viewed as [rows, cols]; mode 0 = the
-    encode's traffic, 1 = the decode's (include/gym_amd.h)."""
+    encode's traffic, 1 = the decode's, | 2 = non-temporal (include/gym_amd.h)."""
     _gpu(a, b)
     if a.dtype != torch.float32 or b.dtype != torch.float32 or min(a.numel(), b.numel()) < rows * cols:
         raise ValueError("probe_chunk_stream: fp32 buffers of rows * cols elements")
