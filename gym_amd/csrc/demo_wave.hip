@@ -369,13 +369,25 @@ __device__ __forceinline__ uint32_t coal_off(int i, int lane, int stride) {
     return (uint32_t)(((lane >> 4) + 4 * i) * stride + 4 * (lane & 15));
 }
 
+// GA_DEMO_NT_LOADS / GA_DEMO_NT_STORES: build options (A/B) for the chunk streams
+#ifndef GA_DEMO_NT_LOADS
+#define GA_DEMO_NT_LOADS 0
+#endif
+#ifndef GA_DEMO_NT_STORES
+#define GA_DEMO_NT_STORES 0
+#endif
 template <typename T, int I0 = 0, int NI = 16>
 __device__ __forceinline__ void load_coal(const T* pb, int stride, bool vec, int lane, float (&o)[16][4]) {
     if (vec) {
 #pragma unroll
         for (int i = I0; i < I0 + NI; ++i)
+#if GA_DEMO_NT_LOADS  // build option (A/B): non-temporal chunk loads
+            Vec4<T>::unpack(stream_load(reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride)))),
+                            o[i]);
+#else
             Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride))),
                             o[i]);
+#endif
     } else {
 #pragma unroll
         for (int i = I0; i < I0 + NI; ++i)
@@ -393,6 +405,8 @@ template <typename T>
 __device__ __forceinline__ void store_vec(T* pb, uint32_t off, const typename Vec4<T>::type& v) {
 #if GA_DEMO_STORE_SC1
     store_sc1(reinterpret_cast<typename Vec4<T>::type*>(pb), off >> 2, v);
+#elif GA_DEMO_NT_STORES  // build option (A/B): non-temporal chunk stores
+    stream_store(reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, off)), v);
 #else
     *reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, off)) = v;
 #endif
