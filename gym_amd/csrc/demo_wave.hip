@@ -1279,18 +1279,21 @@ __device__ __forceinline__ void load_coal_raw(const T* pb, int stride, bool vec,
     }
 }
 
-template <typename T>
+// NTS: the decode's grad stores non-temporal (the 2+-source decode: 1.19 -> 1.13 ms at 350M;
+// the 1-source decode measured 5% slower with them, profiles/r03ac_ab_demo_nt.txt)
+template <typename T, bool NTS = false>
 __device__ __forceinline__ void store_quad(T* pb, int i, int stride, bool vec, int lane, const float (&f)[4]) {
     T* a = at_off(pb, coal_off(i, lane, stride));
     if (vec) {
-        store_vec(pb, coal_off(i, lane, stride), Vec4<T>::pack(f));
+        if constexpr (NTS) stream_store(reinterpret_cast<typename Vec4<T>::type*>(a), Vec4<T>::pack(f));
+        else store_vec(pb, coal_off(i, lane, stride), Vec4<T>::pack(f));
     } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) Elem<T>::store(a + e, f[e]);
     }
 }
 
-template <typename T>
+template <typename T, bool NTS = false>
 __device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, int stride, bool vec, float lr,
                                             int lane, PRaw<T>& raw) {
     if constexpr (sizeof(typename Vec4<T>::type) < 16) {
@@ -1312,7 +1315,7 @@ __device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, in
             for (int i = 0; i < 16; ++i) {
                 const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
                 const float f[4] = {v.x, v.y, v.z, v.w};
-                store_quad(gr, i, stride, vec, lane, f);
+                store_quad<T, NTS>(gr, i, stride, vec, lane, f);
             }
         }
     } else {
@@ -1342,17 +1345,17 @@ __device__ __forceinline__ void sign_update(const float4* tile, T* pr, T* gr, in
             for (int i = 0; i < 16; ++i) {
                 const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
                 const float f[4] = {v.x, v.y, v.z, v.w};
-                store_quad(gr, i, stride, vec, lane, f);
+                store_quad<T, NTS>(gr, i, stride, vec, lane, f);
             }
         }
     }
 }
 
-template <typename T>
+template <typename T, bool NTS = false>
 __device__ __forceinline__ void apply_signs(const float4* tile, T* param, T* grad, int64_t K, int64_t ld, int stride,
                                             bool vec, int nrows, float lr, int lane, PRaw<T>& pre, bool lean = false) {
     if (nrows == 64) {
-        sign_update(tile, param, grad, stride, vec, lr, lane, pre);
+        sign_update<T, NTS>(tile, param, grad, stride, vec, lr, lane, pre);
         if (lean) {  // replicas 1.. a row quad at a time (the updater waves' register budget)
             for (int64_t r = 1; r < K; ++r) {
 #pragma unroll 4
@@ -1382,7 +1385,7 @@ __device__ __forceinline__ void apply_signs(const float4* tile, T* param, T* gra
         for (int64_t r = 1; r < K; ++r) {
             PRaw<T> p;
             load_coal_raw(param + r * ld, stride, vec, lane, p);
-            sign_update(tile, param + r * ld, grad ? grad + r * ld : nullptr, stride, vec, lr, lane, p);
+            sign_update<T, NTS>(tile, param + r * ld, grad ? grad + r * ld : nullptr, stride, vec, lr, lane, p);
         }
         return;
     }
@@ -1656,7 +1659,7 @@ __device__ __forceinline__ void dgroup(const ga_demo_rowgroup& rg, const int32_t
     WAVE_LDS_SYNC();
 }
 
-template <typename T, int MS>
+template <typename T, int MS, bool NTS = false>
 __global__ __launch_bounds__(kThreads) void decode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const ga_demo_rowgroup* __restrict__ groups,
     int ngroups, const float* __restrict__ F64, const int32_t* __restrict__ payload, int64_t pstride, int64_t M,
@@ -1693,8 +1696,8 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
                 td = tens[tix];
                 dchunk_entries(td, (int)job - td.chunk_start, payload, pstride, M, S, cur);
             }
-            apply_signs(reinterpret_cast<const float4*>(W.tile), param + base, grad ? grad + base : nullptr, K, ld,
-                        cols, vec, 64, lr, lane_id(), p0);
+            apply_signs<T, NTS>(reinterpret_cast<const float4*>(W.tile), param + base, grad ? grad + base : nullptr,
+                                K, ld, cols, vec, 64, lr, lane_id(), p0);
             WAVE_LDS_SYNC();
             if (job >= nchunks) break;
             dchunk_params<T>(td, (int)job - td.chunk_start, param, ptr_vec, p0);
@@ -1810,6 +1813,12 @@ static int dec_lc_enabled() {  // GA_DEMO_DECODE_LC=1: the consumer/updater kern
     return e && e[0] == '1' ? 1 : 0;
 }
 
+// GA_DEMO_NT_GRAD=0: plain grad stores at every source count (A/B)
+static int nt_grad_enabled() {
+    const char* e = getenv("GA_DEMO_NT_GRAD");
+    return e && e[0] == '0' ? 0 : 1;
+}
+
 template <typename T, int MS>
 static void launch_decode_ms(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks,
                              const ga_demo_rowgroup* groups, int32_t ngroups, const float* F64,
@@ -1841,8 +1850,12 @@ static void launch_decode_ms(const ga_demo_tensor* tens, int32_t ntens, int32_t 
     const int64_t want = (jobs + kWaves - 1) / kWaves;
     const int grid = (int)(want < resident ? want : resident);
     if (grid <= 0) return;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks, groups, ngroups, F64,
-                       payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
+    if (S >= 2 && nt_grad_enabled())  // several sources: non-temporal grad stores
+        hipLaunchKernelGGL((decode_kernel<T, MS, true>), dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks,
+                           groups, ngroups, F64, payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
+    else
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks, groups, ngroups, F64,
+                           payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
 }
 
 template <typename T>
