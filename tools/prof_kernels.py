@@ -39,7 +39,11 @@ def timed(fn, launches):
         fn()
         b.record()
     torch.cuda.synchronize()
-    return sum(a.elapsed_time(b) for a, b in ev) / launches
+    ts = [a.elapsed_time(b) for a, b in ev]
+    if os.environ.get("GA_PROF_DUMP"):  # per-launch times, for drift over a sustained run
+        with open(os.environ["GA_PROF_DUMP"], "w") as f:
+            f.write("\n".join("%.4f" % t for t in ts) + "\n")
+    return sum(ts) / launches
 
 
 def synth(layout, K, dev, seed=1234):
