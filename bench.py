@@ -143,6 +143,9 @@ class KernelTimer:
         return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else None
 
 
+SUSTAINED_LAUNCHES = 1000  # the headline kernel also timed over ~2 s of back-to-back launches
+
+
 def queued_ms(fn, reps, dev, fill_bytes=1 << 30, fills=4):
     """GPU time per call of fn with its launches queued back to back: streaming
     copies (ga_stream_copy, ~1.5 ms) occupy the GPU while the host enqueues the
@@ -276,6 +279,12 @@ def bench_diloco(args, coll, dev):
         # durations measure; single-launch events add the host's launch gap)
         kern_ms = queued_ms(lambda: eng(reps), max(args.steps, 10), dev)
         kern_how = "HIP events around back-to-back launches queued behind streaming copies (queued_ms)"
+        # the same, sustained for ~2 s: a few steps after idle run faster than a
+        # sustained stream of them (profiles/r03af_diloco_sustained_clocks.txt)
+        # (not under rocprofv3: its kernel statistics stay those of the line's kernel_ms)
+        sus_ms = None if under_profiler() else queued_ms(lambda: eng(reps), SUSTAINED_LAUNCHES, dev)
+    else:
+        sus_ms = None
     K_total = K * coll.world
     n_params = numel(shapes)
     value = K_total * 4 * n_params / t / 1e9
@@ -301,6 +310,8 @@ def bench_diloco(args, coll, dev):
             "kernel": "ga_diloco_outer", "bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),
             "kernel_timing": kern_how,
             "kernel_ms_single_launch_events": round(kern_single, 4) if kern_single is not None else None,
+            "sustained": {"launches": SUSTAINED_LAUNCHES, "kernel_ms": round(sus_ms, 4),
+                          "frac": round(alg_bytes / (sus_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} if sus_ms else None,
             "copy_GBps": round(copy, 1) if copy else None,
             "frac_of_copy": round(achieved / copy, 4) if copy else None},
     }

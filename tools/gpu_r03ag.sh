@@ -17,7 +17,7 @@ for r in 1 2; do
 done
 sleep 20
 echo "S bench $(date +%s.%N)" >> $O/runs.log
-timeout -k 10 300 python bench.py --no-cpu-baseline --no-pmc > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; kill $SMI; exit 1; }
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-pmc --only diloco > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; kill $SMI; exit 1; }
 echo "E bench $(date +%s.%N)" >> $O/runs.log
 python -c "import json; d=json.load(open('$O/bench.json')); print('bench kernel_ms', d['roofline']['kernel_ms'], 'frac', d['roofline']['frac'])"
 kill $SMI
