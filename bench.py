@@ -256,6 +256,16 @@ def stream_copy_rate(dev, nbytes=2 << 30, reps=10):
     return 2 * nbytes / (float(np.median(times)) * 1e-3) / 1e9
 
 
+def stream_copy_sustained(dev, launches, nbytes=2 << 30):
+    """GB/s of the same float4 copy over `launches` back-to-back launches (~2 s)."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(1.0)
+    ms = queued_ms(lambda: ops.stream_copy(src, dst), launches, dev)
+    del src, dst
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
 def bench_diloco(args, coll, dev):
     shapes = MODELS[args.model]()
     layout = ArenaLayout(shapes)
@@ -300,6 +310,7 @@ def bench_diloco(args, coll, dev):
     if coll.world > 1:
         traffic, tnote = None, "not measured at N > 1"
     copy = None if args.pmc_child else stream_copy_rate(dev)
+    copy_sus = stream_copy_sustained(dev, 2 * SUSTAINED_LAUNCHES) if sus_ms else None
     args.copy_GBps = copy
     out = {
         "ms_per_step": t * 1e3, "value": value, "K_total": K_total, "n_params": n_params,
@@ -311,7 +322,9 @@ def bench_diloco(args, coll, dev):
             "kernel_timing": kern_how,
             "kernel_ms_single_launch_events": round(kern_single, 4) if kern_single is not None else None,
             "sustained": {"launches": SUSTAINED_LAUNCHES, "kernel_ms": round(sus_ms, 4),
-                          "frac": round(alg_bytes / (sus_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} if sus_ms else None,
+                          "frac": round(alg_bytes / (sus_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "copy_GBps": round(copy_sus, 1),
+                          "frac_of_copy": round(alg_bytes / (sus_ms * 1e-3) / 1e9 / copy_sus, 4)} if sus_ms else None,
             "copy_GBps": round(copy, 1) if copy else None,
             "frac_of_copy": round(achieved / copy, 4) if copy else None},
     }

@@ -16,6 +16,7 @@ cat $O/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pmc > $O/prof.log 2>&1 || { echo "PROF FAILED"; tail -20 $O/prof.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 bench.py --no-extras --no-cpu-baseline --no-pmc --steps 3 --warmup 1 > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -20 $O/pmc_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 bench.py --no-extras --no-cpu-baseline --no-pmc --steps 3 --warmup 1 > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -20 $O/pmc_write.log; exit 1; }
+grep '^{"metric"' $O/prof.log > $O/bench_under_rocprof.json || echo "no bench line in prof.log"
 python tools/prof_summary.py $O/prof/run_kernel_stats.csv "rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pmc (box $TAG)" > $O/rocprof_stats.txt
 rm -f $O/prof/run_kernel_trace.csv
 python tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write diloco_outer $O/pmc_traffic_diloco.json 9958072320 > $O/pmc_traffic.log 2>&1 || echo "PMC SUMMARY FAILED"
