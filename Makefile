@@ -48,7 +48,7 @@ $(ASAN_LIB): $(SRC) gym_amd/csrc/ga_common.h include/gym_amd.h
 	@echo "ASan runtime: $(ASAN_RT)"
 
 # A kernel variant of the whole library for same-box A/B (tools/ab_lib.sh loads it
-# through GYM_AMD_LIB): make variant VDEFS="-DGA_DEMO_STORE_SC1=1" VNAME=demosc1
+# through GYM_AMD_LIB): make variant VDEFS="-DSOME_FLAG=1" VNAME=name
 VNAME ?= variant
 VDEFS ?=
 variant: build/libgym_amd_$(VNAME).so

@@ -266,6 +266,36 @@ def stream_copy_sustained(dev, launches, nbytes=2 << 30):
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
+def xgmi_block(kind, nbytes, coll_ms, world, step_ms=None, what=None, latency_bound=False):
+    """The SURVEY §8(d) xGMI rooflines of one exchange at `world` GPUs.
+    all_reduce of S bytes (or reduce-scatter + all-gather, the same bytes):
+    bus bytes 2(G-1)/G * S; all_gather of a P-byte per-rank payload: (G-1) * P.
+    Fractions against one 153 GB/s link (the per-link ring model) and against
+    7 links; coll_ms = the collective timed alone, step_ms = the whole step."""
+    G = world
+    bus = (2.0 * (G - 1) / G * nbytes) if kind == "all_reduce" else float((G - 1) * nbytes)
+    out = {"collective": kind, "bytes": int(nbytes), "bus_bytes": int(bus), "world": G,
+           "collective_alone_ms": round(coll_ms, 4) if coll_ms is not None else None}
+    if what:
+        out["what"] = what
+    if G < 2 or coll_ms is None:
+        out["note"] = "world 1 (rehearsal): no bytes cross xGMI, no roofline" if G < 2 else "not timed"
+        return out
+    bw = bus / (coll_ms * 1e-3) / 1e9
+    t_min = bus / (XGMI_LINK_GBS * 1e9) * 1e3
+    out.update({"bus_GBps": round(bw, 1), "t_min_per_link_ring_ms": round(t_min, 4),
+                "frac_per_link_ring": round(bw / XGMI_LINK_GBS, 4),
+                "frac_7link": round(bw / (7 * XGMI_LINK_GBS), 4)})
+    if step_ms is not None:
+        sbw = bus / (step_ms * 1e-3) / 1e9
+        out.update({"bus_GBps_whole_step": round(sbw, 1), "frac_per_link_ring_whole_step": round(sbw / XGMI_LINK_GBS, 4)})
+    if latency_bound:
+        out["bound"] = "latency (a few MB: RCCL's small-message latency, not link bandwidth, sets the time; " \
+                       "reported in microseconds)"
+        out["collective_alone_us"] = round(coll_ms * 1e3, 1)
+    return out
+
+
 def bench_diloco(args, coll, dev):
     shapes = MODELS[args.model]()
     layout = ArenaLayout(shapes)
@@ -328,13 +358,24 @@ def bench_diloco(args, coll, dev):
             "copy_GBps": round(copy, 1) if copy else None,
             "frac_of_copy": round(achieved / copy, 4) if copy else None},
     }
-    if coll.world > 1:
+    if coll.exchange:
+        # the exchange alone: reduce-scatter + all-gather of the whole arena (the bytes of one
+        # all-reduce), unchunked, no kernels; then the step's own bus rate beside it
         S = 4 * n
-        busbw = 2 * (coll.world - 1) / coll.world * S / t / 1e9  # whole step, kernels included
-        out["xgmi"] = {"collective": "reduce_scatter+all_gather (= all-reduce bytes)", "bytes": S,
-                       "bus_GBps_whole_step": round(busbw, 1),
-                       "frac_per_link_ring": round(busbw / XGMI_LINK_GBS, 3),
-                       "frac_7link": round(busbw / (7 * XGMI_LINK_GBS), 3)}
+        full = reps[0, :n]
+        shard = torch.empty(n // coll.world, device=dev)
+        if eng.shard:
+            def exch():
+                coll.reduce_scatter(shard, full)
+                coll.all_gather_into(full, shard)
+        else:
+            def exch():
+                coll.all_reduce_(full)
+        t_x = timed_loop(exch, args.steps, args.warmup, coll)
+        out["xgmi"] = xgmi_block("all_reduce", S, t_x * 1e3, coll.world, step_ms=t * 1e3,
+                                 what="reduce_scatter + all_gather (RCCL) of the arena alone = the bytes of "
+                                      "one all-reduce; the step overlaps it with the sum/update kernels"
+                                 if eng.shard else "all-reduce of the arena alone")
     return out
 
 
@@ -406,7 +447,7 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     # elem -> one element's K values are ceil(4K/64) whole 64-B sectors each way
     sect = (64 + 32) * K * M if layout_kind == "rows" else 2 * 64 * -(-4 * K // 64) * M
     sect += 8 * M if coll.world > 1 else 0  # the packed idx/vals list
-    out = {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
+    out = {"ms_per_step": round(t * 1e3, 4),
            "layout": "[n, K] element-major" if layout_kind == "elem" else "[K, n] rows",
            "K_local": K, "K_total": K * coll.world, "p": p, "selected": M, "alg_bytes": alg,
            "alg_GBps": round(alg / t / 1e9, 1), "sector_bytes": sect, "sector_GBps": round(sect / t / 1e9, 1),
@@ -422,6 +463,12 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
                         "in the step") +
                        ("" if coll.world == 1 else "; every rank draws rank 0's masks from its broadcast generator "
                         f"state: 16 B on the wire instead of the reference's {layout.n} B of masks"))
+    if coll.exchange:  # the packed-value all-reduce alone (~pN fp32, latency-bound)
+        cap = eng.cap
+        t_ar = timed_loop(lambda: coll.all_reduce_(eng.vals[:cap]), args.steps, args.warmup, coll)
+        out["xgmi"] = xgmi_block("all_reduce", 4 * cap, t_ar * 1e3, coll.world, step_ms=t * 1e3,
+                                 what="all-reduce of the packed selected values (capacity pN + 16 sigma + 1024)",
+                                 latency_bound=True)
     if queued is not None:
         out["kernel_ms"] = round(queued, 4)
         out["kernel_alg_GBps"] = round(alg / (queued * 1e-3) / 1e9, 1)
@@ -480,6 +527,23 @@ def bench_simple(args, coll, dev, K_total=8, model="gpt2-char"):
     t = timed_loop(lambda: eng(rs.data), args.steps, args.warmup, coll)
     out = {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
            "K_local": K, "K_total": K * coll.world, "model": model}
+    if coll.exchange:  # the exchange alone: one all-reduce of the arena (RS + AG when sharded)
+        full = rs.data[0, :layout.n]
+        if eng.shard:
+            shard = torch.empty(layout.n // coll.world, device=dev)
+
+            def exch():
+                coll.reduce_scatter(shard, full)
+                coll.all_gather_into(full, shard)
+        else:
+            def exch():
+                coll.all_reduce_(full)
+        t_x = timed_loop(exch, args.steps, args.warmup, coll)
+        S = 4 * layout.n
+        out["xgmi"] = xgmi_block("all_reduce", S, t_x * 1e3, coll.world, step_ms=t * 1e3,
+                                 what=("reduce_scatter + all_gather" if eng.shard else "one all-reduce") +
+                                      f" of the {S / 1e6:.1f} MB gradient arena alone",
+                                 latency_bound=S < (32 << 20))
     if coll.world == 1:  # one ga_replica_mean launch: read K replicas, write K
         q = queued_ms(lambda: eng(rs.data), args.steps, dev)
         alg = 2 * K * 4 * layout.n
@@ -507,9 +571,23 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
         R, C, n1, n2 = codec_view(s, 64)
         flops_one += 2 * (R // n1) * (C // n2) * 2 * 64 ** 3  # two zero-padded 64^3 products per transform
     enc_ms, dec_ms = te.mean_ms(), td.mean_ms()
-    # the decode of 8 gathered payloads (what every GPU runs at 8 nodes), here from
-    # 8 copies of this node's payload: scatter-mean + the dense symmetric inverse
-    gathered8 = codec.payload[0:1].expand(8, -1).contiguous()
+    # the decode of 8 gathered payloads (what every GPU runs at 8 nodes): 8 nodes' own
+    # payloads, each encoded from its own gradient (seeds 7..14) on the shared start,
+    # so every chunk sees up to 8 * 32 distinct coefficients with 1-8 hitters each
+    gathered8 = torch.empty(8, codec.payload.shape[1], dtype=torch.int32, device=dev)
+    Gk, Dk = torch.empty_like(G), torch.empty_like(D)
+    gk = torch.Generator(device=dev)
+    for k in range(8):
+        gk.manual_seed(7 + k)
+        Gk.normal_(0.0, 1e-3, generator=gk)
+        Dk.zero_()
+        ops.demo_encode(plan, P, Gk, Dk, gathered8[k:k + 1], 1e-3, 0.999, 1.0)
+    del Gk, Dk
+    overlap = None
+    if plan.M >= 32000:  # distinct (chunk, coefficient) hits over the 8 payloads, first 1000 chunks of wte
+        e = torch.arange(32000, device=dev) // 32  # wte: 64x64 chunks, k = 32, chunk-local indices
+        key = e[None, :] * 4096 + gathered8[:, :32000].long()
+        overlap = round(float(torch.unique(key).numel()) / key.numel(), 4)
     t8 = KernelTimer()
     dec8 = t8.wrap(lambda: ops.demo_decode(plan, gathered8, P, G, 1e-3))
     t8.on = True
@@ -525,6 +603,21 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
         pipe = PipelinedDeMoCodec(coll, 1, layout, dev, pieces=DEMO_PIECES)
         pipe_ms = timed_loop(lambda: pipe(P, G, D, 1e-3, 0.999, 0.0), args.steps, args.warmup, coll) * 1e3
         del pipe
+    xgmi = None
+    if coll.exchange:  # the payload all-gather alone, (G-1) * P bytes into every GPU
+        ag_ms = timed_loop(codec.exchange, args.steps, args.warmup, coll) * 1e3
+        Pb = codec.payload.numel() * 4
+        step_ms = pipe_ms if pipe_ms is not None else t * 1e3
+        xgmi = xgmi_block("all_gather", Pb, ag_ms, coll.world, step_ms=step_ms,
+                          what=f"all-gather of the packed DeMo payload (int32 idx + fp32 val, {Pb / 1e6:.1f} MB "
+                               f"per rank) alone")
+        # how much of it the step hides behind the codec kernels: the step's time beyond
+        # encode + decode, against the all-gather alone
+        exposed = max(0.0, step_ms - (enc_ms + dec_ms))
+        xgmi["codec_kernels_ms"] = round(enc_ms + dec_ms, 4)
+        xgmi["exposed_ms"] = round(exposed, 4)
+        xgmi["hidden_frac"] = round(max(0.0, min(1.0, 1.0 - exposed / ag_ms)), 4) if ag_ms > 0 else None
+        xgmi["step"] = "pipelined over tensor groups (async RCCL)" if pipe_ms is not None else "one exchange"
     n = numel(shapes)
     copy = getattr(args, "copy_GBps", None)
     # the encode's access-pattern floor on this box: the chunk kernels' 64x64 traffic with no
@@ -543,6 +636,8 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
             "ms_per_step_pipelined": round(pipe_ms, 4) if pipe_ms is not None else None,
             "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4), "decode_8src_ms": round(dec8_ms, 4),
             "decode_nograd_ms": round(tn.mean_ms(), 4),
+            "decode_8src_input": "8 distinct nodes' payloads (own gradients, seeds 7..14)",
+            "decode_8src_distinct_entry_frac": overlap,
             "encode_HBM_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
             "decode_HBM_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
             "decode_8src_HBM_GBps": round((dec_bytes + 7 * 8 * plan.M) / (dec8_ms * 1e-3) / 1e9, 1),
@@ -565,7 +660,7 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
                         "non-temporal streams (the faster counts); frac = floor / encode time.  (The decode's "
                         "pattern probed this way ran slower than the 1-source decode itself, so it is no floor "
                         "and is not reported.)"},
-            "payload_entries": plan.M, "ref_bytes_tx": plan.reference_bytes()}
+            "payload_entries": plan.M, "ref_bytes_tx": plan.reference_bytes(), "xgmi": xgmi}
 
 
 def bench_diloco_torch_gpu(args, coll, dev, fused_ms, model="gpt2-124m", K=8):

@@ -673,11 +673,9 @@ __device__ __forceinline__ const uint32_t* topk_emit(const f32x16& y, const Perm
 }
 
 
+constexpr int kDmEncWaves = 3;  // workgroups per CU the encode is compiled for (register budget ~168 VGPRs, no spills)
 template <typename T>
-#ifndef GA_DEMO_ENC_WAVES
-#define GA_DEMO_ENC_WAVES 3  // workgroups per CU the encode is compiled for (register budget ~168 VGPRs, no spills)
-#endif
-__global__ __launch_bounds__(kDmBlock, GA_DEMO_ENC_WAVES) void demo_encode_kernel(
+__global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const float* __restrict__ F, T* param,
     const T* __restrict__ grad, T* delta, int64_t ld, float lr, float decay, float wd_factor, int32_t* payload,
     int64_t pstride, int64_t M, int ptr_vec) {

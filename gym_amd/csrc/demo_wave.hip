@@ -288,10 +288,7 @@ __device__ __forceinline__ void row_product(const float (&x)[2][8][4], const flo
 // ---- sparse synthesis R = sum_e v_e F[:, b_e] (x) F[:, d_e] in the row-pair layout ----
 // The entries (one per lane where `ent`) as per-parity-of-b lists lstp[par * 64 + i], each
 // padded with a zero entry to whole pairs; np0 / np1 = entry pairs per list.
-#ifndef GA_DEMO_SYNB
-#define GA_DEMO_SYNB 4
-#endif
-constexpr int kSynB = GA_DEMO_SYNB;  // entry pairs per synthesis batch (LDS reads issued ahead of the MFMAs)
+constexpr int kSynB = 4;  // entry pairs per synthesis batch (LDS reads issued ahead of the MFMAs)
 
 __device__ __forceinline__ void parity_lists(uint32_t epos, uint32_t ebits, bool ent, int lane, uint2* lstp,
                                              int& np0, int& np1) {
@@ -369,25 +366,13 @@ __device__ __forceinline__ uint32_t coal_off(int i, int lane, int stride) {
     return (uint32_t)(((lane >> 4) + 4 * i) * stride + 4 * (lane & 15));
 }
 
-// GA_DEMO_NT_LOADS / GA_DEMO_NT_STORES: build options (A/B) for the chunk streams
-#ifndef GA_DEMO_NT_LOADS
-#define GA_DEMO_NT_LOADS 0
-#endif
-#ifndef GA_DEMO_NT_STORES
-#define GA_DEMO_NT_STORES 0
-#endif
 template <typename T, int I0 = 0, int NI = 16>
 __device__ __forceinline__ void load_coal(const T* pb, int stride, bool vec, int lane, float (&o)[16][4]) {
     if (vec) {
 #pragma unroll
         for (int i = I0; i < I0 + NI; ++i)
-#if GA_DEMO_NT_LOADS  // build option (A/B): non-temporal chunk loads
-            Vec4<T>::unpack(stream_load(reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride)))),
-                            o[i]);
-#else
             Vec4<T>::unpack(*reinterpret_cast<const typename Vec4<T>::type*>(at_off(pb, coal_off(i, lane, stride))),
                             o[i]);
-#endif
     } else {
 #pragma unroll
         for (int i = I0; i < I0 + NI; ++i)
@@ -396,20 +381,9 @@ __device__ __forceinline__ void load_coal(const T* pb, int stride, bool vec, int
     }
 }
 
-// GA_DEMO_STORE_SC1 (a build option, A/B): the chunk's vector stores as device-scope
-// (sc1) buffer stores based at the wave-uniform chunk pointer
-#ifndef GA_DEMO_STORE_SC1
-#define GA_DEMO_STORE_SC1 0
-#endif
 template <typename T>
 __device__ __forceinline__ void store_vec(T* pb, uint32_t off, const typename Vec4<T>::type& v) {
-#if GA_DEMO_STORE_SC1
-    store_sc1(reinterpret_cast<typename Vec4<T>::type*>(pb), off >> 2, v);
-#elif GA_DEMO_NT_STORES  // build option (A/B): non-temporal chunk stores
-    stream_store(reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, off)), v);
-#else
     *reinterpret_cast<typename Vec4<T>::type*>(at_off(pb, off)) = v;
-#endif
 }
 
 template <typename T>
@@ -572,11 +546,6 @@ __device__ __forceinline__ void chunk64_tail(const f32x16 (&Y)[2][2], int k, T* 
         }
         WAVE_LDS_SYNC();
     } else {
-#ifdef GA_EXP_NOFALLBACK
-        __builtin_trap();
-    }
-    if (0) {
-#endif
         // more than kCand keys >= T0 (flat spectra, all-zero chunks): exact k-th
         // key over all 4096 keys, ties to the lowest positions, slots in position order.
         // Rare, so written for registers, not speed: every loop re-reads Y through an
@@ -989,207 +958,6 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
     DW_PH_FLUSH();
 }
 
-// ============================================================================
-// Encode, loader / consumer form: the 64x64 chunks of ga_demo_encode_sym.
-//
-// A workgroup of 12 waves per CU (3 per SIMD, <= 168 VGPRs each): 8 CONSUMER
-// waves transform chunks, 4 LOADER waves stream them in.  Loader w feeds
-// consumers w and w + 4 alternately: it loads a chunk's delta and grad
-// (coalesced, 32 KB in registers), forms x = decay * delta + lr * grad, waits
-// for the consumer's LDS slot to be free and writes x into it (the swizzled t4
-// layout).  The consumer never waits on HBM: it reads x from its slot in the
-// row-pair layout, runs both DCT products, the top-k and the residual, leaves
-// delta = x - R in the slot, stores it coalesced and frees the slot.  So the
-// matrix and vector pipes of a SIMD serve two consumers while its loader keeps
-// the next chunk's loads in flight -- instead of every wave alternating
-// between waiting on its own loads and computing (the all-in-one kernel
-// above, two waves per SIMD).
-// Hand-off: one LDS word per slot, 2i + 1 = chunk i written, 2i + 2 = chunk i
-// consumed (0 initially); a wave's LDS operations execute in order, so a word
-// written after the data is seen only after the data.
-// The arithmetic per chunk is chunk64's (same x rounding, same products, same
-// top-k and residual), so the results are identical to the all-in-one kernel.
-// ============================================================================
-__device__ __forceinline__ int64_t chunk_base(const ga_demo_tensor& td, int c);
-__device__ __forceinline__ bool chunk_vec(const ga_demo_tensor& td, int ptr_vec);
-
-constexpr int kCons = 8;
-constexpr int kLoaders = 4;
-constexpr int kLcThreads = 64 * (kCons + kLoaders);
-
-struct LcLDS {
-    float Hb[32 * kLd];
-    float4 slot[kCons][64 * 16];
-    ListLDS lists[kCons];
-    int flag[kCons];
-};
-
-__device__ __forceinline__ void lds_wait_flag(const int* f, int want) {
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != want) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ void lds_set_flag(int* f, int v) {
-    asm volatile("" ::: "memory");
-    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// A wave's chunk sequence job0, job0 + stride, ... as (replica, chunk) pairs, advanced
-// with scalar arithmetic (no 64-bit division per chunk)
-struct LcCursor {
-    int64_t rep;
-    int chunk;
-    __device__ __forceinline__ LcCursor(int64_t job, int nchunks) {
-        rep = job / nchunks;
-        chunk = (int)(job - rep * nchunks);
-    }
-    __device__ __forceinline__ void advance(int64_t stride, int nchunks) {
-        const int64_t r = stride / nchunks;  // uniform; stride < nchunks in practice
-        rep += r;
-        chunk += (int)(stride - r * nchunks);
-        if (chunk >= nchunks) {
-            chunk -= nchunks;
-            ++rep;
-        }
-    }
-};
-
-struct LcJob {
-    ga_demo_tensor td;
-    int c;         // chunk within the tensor
-    int64_t base;  // element offset of the chunk's (0, 0) in its replica
-    bool vec;
-};
-
-__device__ __forceinline__ LcJob lc_job(const ga_demo_tensor* __restrict__ tens, int ntens, int chunk, int ptr_vec) {
-    LcJob j;
-    j.td = tens[find_tensor(tens, ntens, -1, chunk)];
-    j.c = chunk - j.td.chunk_start;
-    j.base = chunk_base(j.td, j.c);
-    j.vec = chunk_vec(j.td, ptr_vec);
-    return j;
-}
-
-template <typename T>
-__global__ __launch_bounds__(kLcThreads) void encode_lc_kernel(
-    const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const float* __restrict__ F64, T* param0,
-    const T* __restrict__ grad0, T* delta0, int64_t ld, int64_t K, float lr, float decay, float wd_factor,
-    int32_t* payload0, int64_t pstride, int64_t M, int ptr_vec) {
-    __shared__ LcLDS L;
-    for (int q = threadIdx.x; q < 32 * 64; q += kLcThreads) L.Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
-    if (threadIdx.x < kCons) L.flag[threadIdx.x] = 0;
-    __syncthreads();
-    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int64_t n64 = (int64_t)nchunks * K;
-    const int64_t stride = (int64_t)gridDim.x * kCons;
-    if (wid < kCons) {  // ---- consumer
-        const int cw = wid;
-        float4* tile = L.slot[cw];
-        int i = 0;
-        LcCursor cur((int64_t)blockIdx.x * kCons + cw, nchunks);
-        for (int64_t job = (int64_t)blockIdx.x * kCons + cw; job < n64; job += stride, ++i, cur.advance(stride, nchunks)) {
-            const LcJob j = lc_job(tens, ntens, cur.chunk, ptr_vec);
-            const int64_t rep = cur.rep;
-            int32_t* pi = payload0 + rep * pstride + j.td.payload_off + (int64_t)j.c * j.td.k;
-            float* pv = reinterpret_cast<float*>(payload0 + rep * pstride + M) + j.td.payload_off + (int64_t)j.c * j.td.k;
-            lds_wait_flag(&L.flag[cw], 2 * i + 1);
-            const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-            f32x16 Y[2][2];  // [parity of b][qc]
-            {
-                f32x16 Tm[2][2];
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    float xs[8][4];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        const float4 v = tile[t4(s2 ? 63 - l : l, blk(h, q))];
-                        xs[q][0] = v.x;
-                        xs[q][1] = v.y;
-                        xs[q][2] = v.z;
-                        xs[q][3] = v.w;
-                    }
-                    row_product_half(xs, L.Hb, l, h, Tm[s2]);
-                }
-#pragma unroll
-                for (int qc = 0; qc < 2; ++qc) {
-#pragma unroll
-                    for (int par = 0; par < 2; ++par) {
-                        f32x16 acc = zero16();
-#pragma unroll
-                        for (int t = 0; t < 16; ++t) {
-                            const float u = Tm[0][qc][t], w = Tm[1][qc][t];
-                            acc = mfma(L.Hb[rowmap(t, h) * kLd + 2 * l + par], par ? u - w : u + w, acc);
-                        }
-                        Y[par][qc] = acc;
-                    }
-                }
-            }
-#ifdef GA_DEMO_STAMPS
-            unsigned long long ph_acc[16] = {}, ph_last = 0;
-#endif
-            chunk64_tail<T>(Y, j.td.k, delta0 + rep * ld + j.base, j.td.cols, j.vec, pi, pv, L.Hb, L.lists[cw], tile
-#ifdef GA_DEMO_STAMPS
-                            , ph_acc, ph_last
-#endif
-            );
-            lds_set_flag(&L.flag[cw], 2 * i + 2);
-        }
-    } else {  // ---- loader: consumers lw and lw + kLoaders, alternately
-        const int lw = wid - kCons;
-        __builtin_amdgcn_s_setprio(1);
-        LcCursor curs[2] = {LcCursor((int64_t)blockIdx.x * kCons + lw, nchunks),
-                            LcCursor((int64_t)blockIdx.x * kCons + lw + kLoaders, nchunks)};
-        for (int i = 0;; ++i) {
-            bool any = false;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int cw = lw + u * kLoaders;
-                const int64_t job = (int64_t)blockIdx.x * kCons + cw + (int64_t)i * stride;
-                if (job >= n64) continue;
-                any = true;
-                const LcJob j = lc_job(tens, ntens, curs[u].chunk, ptr_vec);
-                const int64_t rep = curs[u].rep;
-                curs[u].advance(stride, nchunks);
-                const int lane = lane_id();
-                T* prm = param0 + rep * ld + j.base;
-                if (wd_factor != 1.f) {  // decoupled weight decay of p (demo.py:159-160), its own pass
-                    float pw[16][4];
-                    load_coal(prm, j.td.cols, j.vec, lane, pw);
-#pragma unroll
-                    for (int q = 0; q < 16; ++q)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) pw[q][e] *= wd_factor;
-                    store_coal(prm, j.td.cols, j.vec, lane, pw);
-                }
-                float Dv[16][4], Gv[16][4];
-                load_coal(delta0 + rep * ld + j.base, j.td.cols, j.vec, lane, Dv);
-                load_coal(grad0 + rep * ld + j.base, j.td.cols, j.vec, lane, Gv);
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) Dv[q][e] = fmaf(lr, Gv[q][e], Dv[q][e] * decay);  // as chunk64
-                lds_wait_flag(&L.flag[cw], 2 * i);
-                float4* tile = L.slot[cw];
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    tile[t4((lane >> 4) + 4 * q, lane & 15)] = make_float4(Dv[q][0], Dv[q][1], Dv[q][2], Dv[q][3]);
-                lds_set_flag(&L.flag[cw], 2 * i + 1);
-            }
-            if (!any) break;
-        }
-    }
-}
-
-// GA_DEMO_ENCODE_LC=1 selects the loader/consumer kernel for the 64x64 chunks (opt-in:
-// measured 1-4% slower than the all-in-one kernel for the encode and both decodes on
-// one box, profiles/r03d_ab_demo_lc.txt -- the two consumer waves per SIMD that LDS
-// allows are the all-in-one kernel's two waves, and their issue, not the loads, sets
-// the time; read at every launch)
-static int lc_enabled() {
-    const char* e = getenv("GA_DEMO_ENCODE_LC");
-    return e && e[0] == '1' ? 1 : 0;
-}
-
 template <typename T>
 static int launch(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, const ga_demo_rowgroup* groups,
                   int32_t ngroups, const float* F64, void* param, const void* grad, void* delta, int64_t K,
@@ -1201,16 +969,6 @@ static int launch(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks, co
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         return n > 0 ? n : 256;
     }();
-    const bool lc = lc_enabled() && nchunks > 0;
-    if (lc) {  // 64x64 chunks: loader / consumer kernel, one workgroup per CU
-        const int64_t want = ((int64_t)nchunks * K + kCons - 1) / kCons;
-        const int grid = (int)(want < cus ? want : cus);
-        hipLaunchKernelGGL(encode_lc_kernel<T>, dim3(grid), dim3(kLcThreads), 0, stream, tens, ntens, nchunks, F64,
-                           (T*)param, (const T*)grad, (T*)delta, ld, K, lr, decay, wd_factor, payload, pstride, M,
-                           ptr_vec);
-        if (ngroups == 0) return GA_OK;
-        nchunks = 0;  // the row groups: the all-in-one kernel below
-    }
     auto kern = encode_kernel<T>;
     static const int resident = [&] {
         int per_cu = 0;
@@ -1709,135 +1467,11 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     }
 }
 
-// ============================================================================
-// Decode, consumer / updater form (64x64 chunks, S <= 8 sources): the same
-// split as the encode's loader / consumer kernel.  Per workgroup (one per CU,
-// 12 waves, <= 168 VGPRs): 8 CONSUMER waves turn a chunk's gathered entries
-// into sign(g) in their LDS slot (dchunk_signs: scatter-mean + inverse DCT, the
-// next chunk's entries already in flight), 4 UPDATER waves, each serving
-// consumers u and u + 4, hold the replica-0 parameters of both consumers' next
-// chunks in registers (loaded a whole chunk ahead), wait for the signs, run
-// p -= lr * sign and grad = sign for every replica and free the slot.  The
-// consumers never wait on HBM; the updaters never wait on the transform while
-// there is a chunk to store.  Same per-chunk arithmetic as decode_kernel.
-// Slot words: 2i = free for chunk i, 2i + 1 = chunk i's signs written.
-// ============================================================================
-constexpr int kUpd = 4;
-
-struct DecLcLDS {
-    float Hb[32 * kLd];
-    DecLDS slot[kCons];
-    int flag[kCons];
-};
-
-template <typename T, int MS>
-__global__ __launch_bounds__(kLcThreads) void decode_lc_kernel(
-    const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const float* __restrict__ F64,
-    const int32_t* __restrict__ payload, int64_t pstride, int64_t M, int S, T* param, T* grad, int64_t K, int64_t ld,
-    float lr, int ptr_vec) {
-    static_assert(kCons + kUpd == kLcThreads / 64, "12 waves: 8 consumers, 4 updaters");
-    __shared__ DecLcLDS L;
-    for (int q = threadIdx.x; q < 32 * 64; q += kLcThreads) L.Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
-    if (threadIdx.x < kCons) L.flag[threadIdx.x] = 0;
-    __syncthreads();
-    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int64_t stride = (int64_t)gridDim.x * kCons;
-    if (wid < kCons) {  // ---- consumer
-        const int cw = wid;
-        DecLDS& W = L.slot[cw];
-        int64_t job = (int64_t)blockIdx.x * kCons + cw;
-        if (job >= nchunks) return;
-        // a chunk's entries start at e0 = payload_off + c * k of its tensor
-        auto entries_at = [&](int64_t j, int& k, int64_t& e0) {
-            const int t = find_tensor(tens, ntens, -1, (int)j);
-            k = tens[t].k;
-            e0 = tens[t].payload_off + (int64_t)((int)j - tens[t].chunk_start) * k;
-        };
-        int k;
-        int64_t e0;
-        entries_at(job, k, e0);
-        DecIn<MS> cur;
-        dchunk_entries_at<MS>(k, e0, payload, pstride, M, S, cur);
-        for (int i = 0;; ++i) {
-            const int64_t nj = job + stride;
-            const bool more = nj < nchunks;
-            int kn = k;
-            int64_t e0n = e0;
-            if (more) entries_at(nj, kn, e0n);
-            // the next chunk's entries, in flight behind this transform (none past the end:
-            // every slot is still written, so the struct stays in registers)
-            DecIn<MS> nxt;
-            dchunk_entries_at<MS>(kn, e0n, payload, pstride, M, more ? S : 0, nxt);
-            lds_wait_flag(&L.flag[cw], 2 * i);
-            dchunk_signs(k, S, cur, L.Hb, W);
-            lds_set_flag(&L.flag[cw], 2 * i + 1);
-            if (!more) break;
-            job = nj;
-            k = kn;
-            e0 = e0n;
-            cur = nxt;
-        }
-    } else {  // ---- updater: consumers uw and uw + kUpd, alternately
-        // the replica-0 parameters of the chunk it serves next are loaded (into pr) right
-        // after the previous chunk's stores, so they arrive while that consumer transforms
-        const int uw = wid - kCons;
-        __builtin_amdgcn_s_setprio(1);
-        int64_t job[2] = {(int64_t)blockIdx.x * kCons + uw, (int64_t)blockIdx.x * kCons + uw + kUpd};
-        int i_of[2] = {0, 0};
-        int u = 0;
-        if (job[0] >= nchunks) return;
-        ga_demo_tensor td = tens[find_tensor(tens, ntens, -1, (int)job[0])];
-        PRaw<T> pr;
-        dchunk_params<T>(td, (int)job[0] - td.chunk_start, param, ptr_vec, pr);
-        while (true) {
-            const int cw = uw + u * kUpd;
-            const int64_t base = chunk_base(td, (int)job[u] - td.chunk_start);
-            lds_wait_flag(&L.flag[cw], 2 * i_of[u] + 1);
-            apply_signs(reinterpret_cast<const float4*>(L.slot[cw].tile), param + base, grad ? grad + base : nullptr,
-                        K, ld, td.cols, chunk_vec(td, ptr_vec), 64, lr, lane_id(), pr, true);
-            lds_set_flag(&L.flag[cw], 2 * i_of[u] + 2);
-            job[u] += stride;
-            ++i_of[u];
-            // the other consumer's turn, unless its sequence has ended (then this one's)
-            const int nu = job[1 - u] < nchunks ? 1 - u : u;
-            if (job[nu] >= nchunks) break;
-            u = nu;
-            td = tens[find_tensor(tens, ntens, -1, (int)job[u])];
-            dchunk_params<T>(td, (int)job[u] - td.chunk_start, param, ptr_vec, pr);
-        }
-    }
-}
-
-static int dec_lc_enabled() {  // GA_DEMO_DECODE_LC=1: the consumer/updater kernel (opt-in, see the encode's)
-    const char* e = getenv("GA_DEMO_DECODE_LC");
-    return e && e[0] == '1' ? 1 : 0;
-}
-
-// GA_DEMO_NT_GRAD=0: plain grad stores at every source count (A/B)
-static int nt_grad_enabled() {
-    const char* e = getenv("GA_DEMO_NT_GRAD");
-    return e && e[0] == '0' ? 0 : 1;
-}
-
 template <typename T, int MS>
 static void launch_decode_ms(const ga_demo_tensor* tens, int32_t ntens, int32_t nchunks,
                              const ga_demo_rowgroup* groups, int32_t ngroups, const float* F64,
                              const int32_t* payload, int64_t pstride, int64_t M, int S, void* param, void* grad,
                              int64_t K, int64_t ld, float lr, int ptr_vec, hipStream_t stream) {
-    if constexpr (MS == 8) if (nchunks > 0 && dec_lc_enabled()) {  // 64x64 chunks: consumer / updater kernel
-        static const int cus = [] {
-            int dev = 0, n = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-            return n > 0 ? n : 256;
-        }();
-        const int64_t want = ((int64_t)nchunks + kCons - 1) / kCons;
-        const int g = (int)(want < cus ? want : cus);
-        hipLaunchKernelGGL((decode_lc_kernel<T, MS>), dim3(g), dim3(kLcThreads), 0, stream, tens, ntens, nchunks, F64,
-                           payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
-        if (ngroups == 0) return;
-        nchunks = 0;  // the row groups: decode_kernel below
-    }
     auto kern = decode_kernel<T, MS>;
     static const int resident = [&] {
         int per_cu = 0, dev = 0, cus = 0;
@@ -1850,7 +1484,7 @@ static void launch_decode_ms(const ga_demo_tensor* tens, int32_t ntens, int32_t 
     const int64_t want = (jobs + kWaves - 1) / kWaves;
     const int grid = (int)(want < resident ? want : resident);
     if (grid <= 0) return;
-    if (S >= 2 && nt_grad_enabled())  // several sources: non-temporal grad stores
+    if (S >= 2)  // several sources: non-temporal grad stores
         hipLaunchKernelGGL((decode_kernel<T, MS, true>), dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks,
                            groups, ngroups, F64, payload, pstride, M, S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
     else

@@ -73,44 +73,25 @@ template <> struct Vec4<__hip_bfloat16> {
 // Non-temporal (streaming) vector loads and stores for data touched once per
 // launch: a float4 copy of 4.6 GiB runs 5.96 TB/s with both hinted against
 // 5.67 TB/s plain (tools/ubench_copy_nt.hip, profiles/r02z_ubench_copy_nt.txt).
-#ifndef GA_STREAM_NT
-#define GA_STREAM_NT 1
-#endif
 typedef float ga_f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int ga_u2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float4 stream_load(const float4* p) {
-#if GA_STREAM_NT
     const ga_f4 v = __builtin_nontemporal_load(reinterpret_cast<const ga_f4*>(p));
     return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
 }
 __device__ __forceinline__ uint2 stream_load(const uint2* p) {
-#if GA_STREAM_NT
     const ga_u2 v = __builtin_nontemporal_load(reinterpret_cast<const ga_u2*>(p));
     return make_uint2(v.x, v.y);
-#else
-    return *p;
-#endif
 }
 __device__ __forceinline__ void stream_store(float4* p, const float4& v) {
-#if GA_STREAM_NT
     ga_f4 w;
     w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
     __builtin_nontemporal_store(w, reinterpret_cast<ga_f4*>(p));
-#else
-    *p = v;
-#endif
 }
 __device__ __forceinline__ void stream_store(uint2* p, const uint2& v) {
-#if GA_STREAM_NT
     ga_u2 w;
     w.x = v.x; w.y = v.y;
     __builtin_nontemporal_store(w, reinterpret_cast<ga_u2*>(p));
-#else
-    *p = v;
-#endif
 }
 
 // Device-scope (sc1) vector stores for streams written once per launch: the

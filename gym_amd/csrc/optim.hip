@@ -14,9 +14,6 @@
 // gradient is written back.
 #include "ga_common.h"
 
-#ifndef GA_ADAM_STORE_SC1
-#define GA_ADAM_STORE_SC1 1
-#endif
 
 namespace ga {
 
@@ -70,16 +67,10 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ par
         float pp[4] = {p.x, p.y, p.z, p.w}, mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], ap);
-#if GA_ADAM_STORE_SC1  // build option (A/B): device-scope buffer stores based at the workgroup's block
         const uint32_t o = (uint32_t)(i - lo);
         store_sc1(reinterpret_cast<float4*>(param) + lo, o, make_float4(pp[0], pp[1], pp[2], pp[3]));
         store_sc1(reinterpret_cast<float4*>(m_) + lo, o, make_float4(mm[0], mm[1], mm[2], mm[3]));
         store_sc1(reinterpret_cast<float4*>(v_) + lo, o, make_float4(vv[0], vv[1], vv[2], vv[3]));
-#else
-        stream_store(reinterpret_cast<float4*>(param) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
-        stream_store(reinterpret_cast<float4*>(m_) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
-        stream_store(reinterpret_cast<float4*>(v_) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
-#endif
     }
     // scalar tail (n % 4), handled by the last workgroup
     if (blockIdx.x == gridDim.x - 1) {

@@ -13,8 +13,6 @@
 // depend on the launch geometry.  dst may alias src (in-place average): each
 // lane reads every replica of its vector before it writes any, and no two
 // lanes touch the same vector, so the sources carry no __restrict__.
-#include <stdlib.h>
-
 #include "ga_common.h"
 
 namespace ga {
@@ -98,7 +96,7 @@ __device__ __forceinline__ float outer_update(float sum, float& master, float& b
     return master;
 }
 
-template <typename T, typename M, bool VEC, bool SC1 = false>
+template <typename T, typename M, bool VEC>
 __global__ __launch_bounds__(kBlock) void diloco_outer_kernel(
     const T* src, int64_t K, int64_t ld_src, int64_t n, M* master, M* mom,
     OuterParams op, T* dst, int64_t K_out, int64_t ld_dst) {
@@ -124,16 +122,11 @@ __global__ __launch_bounds__(kBlock) void diloco_outer_kernel(
 #pragma unroll
             for (int e = 0; e < 4; ++e) out[e] = outer_update(acc[e], m[e], b[e], op);
             const V o = Vec4<T>::pack(out);
-            if constexpr (SC1) {  // the workgroup's block of each stream as the store base
-                const uint32_t i = (uint32_t)(v - lo);
-                store_sc1(reinterpret_cast<VM*>(master) + lo, i, Vec4<M>::pack(m));
-                if (has_mom) store_sc1(reinterpret_cast<VM*>(mom) + lo, i, Vec4<M>::pack(b));
-                for (int64_t j = 0; j < K_out; ++j) store_sc1(reinterpret_cast<V*>(dst + j * ld_dst) + lo, i, o);
-            } else {
-                stream_store(reinterpret_cast<VM*>(master) + v, Vec4<M>::pack(m));
-                if (has_mom) stream_store(reinterpret_cast<VM*>(mom) + v, Vec4<M>::pack(b));
-                for (int64_t j = 0; j < K_out; ++j) stream_store(reinterpret_cast<V*>(dst + j * ld_dst) + v, o);
-            }
+            // device-scope (sc1) stores based at the workgroup's block of each stream
+            const uint32_t i = (uint32_t)(v - lo);
+            store_sc1(reinterpret_cast<VM*>(master) + lo, i, Vec4<M>::pack(m));
+            if (has_mom) store_sc1(reinterpret_cast<VM*>(mom) + lo, i, Vec4<M>::pack(b));
+            for (int64_t j = 0; j < K_out; ++j) store_sc1(reinterpret_cast<V*>(dst + j * ld_dst) + lo, i, o);
         }
     } else {
         chunk_range(n, lo, hi);
@@ -149,12 +142,6 @@ __global__ __launch_bounds__(kBlock) void diloco_outer_kernel(
             for (int64_t j = 0; j < K_out; ++j) Elem<T>::store(dst + j * ld_dst + i, out);
         }
     }
-}
-
-// GA_STORE_SC1=0: the nt vector stores instead of the sc1 buffer stores (A/B)
-static bool store_sc1_enabled() {
-    const char* e = getenv("GA_STORE_SC1");
-    return !(e && e[0] == '0');
 }
 
 static bool aligned(const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; }
@@ -187,11 +174,7 @@ static int launch_diloco(const void* src, int64_t K, int64_t ld_src, int64_t n, 
     const bool vec = (n % 4 == 0) && (ld_src % 4 == 0) && (ld_dst % 4 == 0) &&
                      aligned(src, vb) && aligned(dst, vb) && aligned(master, vm) &&
                      aligned(mom, vm);
-    if (vec && store_sc1_enabled()) {
-        hipLaunchKernelGGL((diloco_outer_kernel<T, M, true, true>), dim3(chunk_grid(n / 4)),
-                           dim3(kBlock), 0, stream, (const T*)src, K, ld_src, n, (M*)master,
-                           (M*)mom, op, (T*)dst, K_out, ld_dst);
-    } else if (vec) {
+    if (vec) {
         hipLaunchKernelGGL((diloco_outer_kernel<T, M, true>), dim3(chunk_grid(n / 4)),
                            dim3(kBlock), 0, stream, (const T*)src, K, ld_src, n, (M*)master,
                            (M*)mom, op, (T*)dst, K_out, ld_dst);

@@ -22,7 +22,6 @@
 // (one 24-bit draw per element): the mask no longer bounds the kernel.
 #include <math.h>
 
-#include <atomic>
 
 #include "ga_common.h"
 
@@ -31,10 +30,7 @@ namespace ga {
 constexpr int kSpBlock = 256;
 constexpr int kSpPerThread = 64;                       // elements per lane: one Philox group
 constexpr int kSpTile = kSpBlock * kSpPerThread;       // 16384 elements per workgroup
-#ifndef GA_SP_SELCAP
-#define GA_SP_SELCAP 4096
-#endif
-constexpr int kSelCap = GA_SP_SELCAP;                  // selected positions listed per window
+constexpr int kSelCap = 4096;                  // selected positions listed per window
 constexpr int kScanBlock = 1024;
 constexpr int kGapTable = 64;
 
@@ -348,14 +344,8 @@ struct FastDiv {
 //   [n, ld] element-major (ei = ld >= K, ek = 1): consecutive lanes read the K
 //     replicas of ONE element, i.e. one element's K=32 fp32 values are one
 //     128-B line -- the gather/write-back moves whole lines.
-#ifndef GA_SP_SLOTS
-#define GA_SP_SLOTS 2048
-#endif
-#ifndef GA_SP_SLOTS_V4
-#define GA_SP_SLOTS_V4 3072
-#endif
-constexpr int kGatherSlots = GA_SP_SLOTS;  // floats of LDS for the (element, replica) values
-constexpr int kGatherSlotsV4 = GA_SP_SLOTS_V4;  // the same for the 4-replica vector form
+constexpr int kGatherSlots = 2048;  // floats of LDS for the (element, replica) values
+constexpr int kGatherSlotsV4 = 3072;  // the same for the 4-replica vector form
 // (measured, K = 32: 2048 slots 0.058-0.060 ms, 3072 0.053-0.056 ms, 4096 0.055-0.056 ms)
 // (measured, K = 32 element-major: 2048 slots 0.075 ms, 4096 slots 0.090 ms -- the
 // 16 loads in flight per lane cost 95 VGPRs and occupancy; 3072: 0.097-0.107 ms)
@@ -547,15 +537,10 @@ __global__ __launch_bounds__(kSpBlock) void sparta_select_kernel(Pred P, int64_t
 // mask while tile t's loads are in flight ran 0.062 / 0.065 / 0.074 ms at 2 / 4 /
 // 8 tiles per wave (fewer waves in flight), and builds of the kernel with only
 // its mask (0.015 ms) or only its gather (0.034 ms) add up to the whole.
-#ifndef GA_SP_GROUPS
-#define GA_SP_GROUPS 1  // 64-element groups per lane (2: no faster, profiles/r02x_ab_sparta_groups.txt)
-#endif
-constexpr int kWGroups = GA_SP_GROUPS;
+constexpr int kWGroups = 1;  // 64-element groups per lane (2: no faster, profiles/r02x_ab_sparta_groups.txt)
 constexpr int kWTile = 64 * kSpPerThread * kWGroups;  // elements per wavefront tile
 constexpr int kWList = 256;                // listed positions per window
-#ifndef GA_SP_WAVES
-#define GA_SP_WAVES 4  // wavefronts (independent tiles) per workgroup
-#endif
+constexpr int kSpWaves = 4;  // wavefronts (independent tiles) per workgroup
 
 // orders this wave's LDS accesses (the wave is the only writer of its slices)
 __device__ __forceinline__ void wave_sync() {
@@ -573,12 +558,9 @@ __device__ __forceinline__ void wave_sync() {
 // non-temporally (0.045 -> 0.041 ms, profiles/r02z_ab_sparta_nt.txt).  An LDS-staged form (values written at an
 // odd stride, summed by one lane per element) measured 5% slower
 // (profiles/r02x_ab_sparta_batch.txt).
-#ifndef GA_SP_DPP_PASSES
-#define GA_SP_DPP_PASSES 8
-#endif
 template <typename T, int KQ>
 struct WaveBatchDpp {
-    static constexpr int K = 4 * KQ, EPP = 64 / KQ, NP = GA_SP_DPP_PASSES, EB = NP * EPP;
+    static constexpr int K = 4 * KQ, EPP = 64 / KQ, NP = 8, EB = NP * EPP;
     using V = typename Vec4<T>::type;
     __device__ __forceinline__ static float shr1(float a) {  // lane i <- lane i - 1 within each 16-lane row
         return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x111, 0xf, 0xf, true));
@@ -610,33 +592,6 @@ struct WaveBatchDpp {
             }
             const int64_t pos = pos0 + b0 + e;
             if (q == KQ - 1 && e < ne && pos < cap) Elem<T>::store(vals + pos, a);
-        }
-    }
-    // the same sums into LDS: out[b0 + e] (the one-pass select writes them after its look-back)
-    __device__ __forceinline__ static void sums_lds(const T* src, int64_t ld, int64_t tile0, const uint16_t* list,
-                                                    int b0, int ne, int lane, float* out) {
-        const int q = lane % KQ, el = lane / KQ;
-        V v[NP];
-#pragma unroll
-        for (int u = 0; u < NP; ++u) {
-            const int e = u * EPP + el;
-            if (e < ne) v[u] = stream_load(reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * q));
-        }
-#pragma unroll
-        for (int u = 0; u < NP; ++u) {
-            if (u * EPP >= ne) break;  // wave-uniform
-            const int e = u * EPP + el;
-            float f[4] = {0.f, 0.f, 0.f, 0.f};
-            if (e < ne) Vec4<T>::unpack(v[u], f);
-            float a = 0.f;
-#pragma unroll
-            for (int s = 0; s < KQ; ++s) {
-                float left = KQ > 1 ? shr1(a) : 0.f;
-                if (q == 0) left = 0.f;
-                const float c = (((left + f[0]) + f[1]) + f[2]) + f[3];
-                a = q == s ? c : a;
-            }
-            if (q == KQ - 1 && e < ne) out[b0 + e] = a;
         }
     }
     __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0,
@@ -674,20 +629,17 @@ struct WaveBatchDpp {
 // 8 waves per SIMD: the per-source instantiations fit 64 VGPRs without spills
 // (67 / 63 unconstrained); Philox mode 0.048 -> 0.045 ms, reference draw
 // unchanged (profiles/r02z_ab_sparta_split_wpe.txt)
-#ifndef GA_SP_WPE
-#define GA_SP_WPE 8
-#endif
-#define GA_SP_WPE_ATTR __attribute__((amdgpu_waves_per_eu(GA_SP_WPE, GA_SP_WPE)))
+#define GA_SP_WPE_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 template <typename T, int KQ, int SRC>
-__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_average_wave_kernel(Pred P, int64_t n, T* __restrict__ src,
+__global__ __launch_bounds__(64 * kSpWaves) GA_SP_WPE_ATTR void sparta_average_wave_kernel(Pred P, int64_t n, T* __restrict__ src,
                                                                                int64_t ld, float divisor) {
     using B = WaveBatchDpp<T, KQ>;
     __shared__ uint64_t tab[kGapTable];
-    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
+    __shared__ uint16_t lists[kSpWaves][kWList];
     if (SRC != 1) load_gap_table(P, tab);  // the reference draw has no gap table
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint16_t* list = lists[wid];
-    const int64_t t = (int64_t)blockIdx.x * GA_SP_WAVES + wid;
+    const int64_t t = (int64_t)blockIdx.x * kSpWaves + wid;
     const int64_t tile0 = t * kWTile;
     // lane owns the kWGroups consecutive 64-element groups from e0 (ascending over lanes)
     const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread * kWGroups;
@@ -742,16 +694,16 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_averag
 // At p = 0.005 a tile lists ~20 elements: 20 x K words per wave, with no workgroup
 // barrier between the mask draw and the gathers.
 constexpr int kRowsKB = 32;
-constexpr int kRTile = 64 * kSpPerThread;  // one 64-element group per lane, whatever GA_SP_GROUPS is
+constexpr int kRTile = 64 * kSpPerThread;  // one 64-element group per lane, whatever kWGroups is
 template <typename T, int SRC>
-__global__ __launch_bounds__(64 * GA_SP_WAVES) void sparta_average_rows_wave_kernel(Pred P, int64_t n, T* src,
+__global__ __launch_bounds__(64 * kSpWaves) void sparta_average_rows_wave_kernel(Pred P, int64_t n, T* src,
                                                                                     int64_t ld, int K, float divisor) {
     __shared__ uint64_t tab[kGapTable];
-    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
+    __shared__ uint16_t lists[kSpWaves][kWList];
     if (SRC != 1) load_gap_table(P, tab);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint16_t* list = lists[wid];
-    const int64_t tile0 = ((int64_t)blockIdx.x * GA_SP_WAVES + wid) * kRTile;
+    const int64_t tile0 = ((int64_t)blockIdx.x * kSpWaves + wid) * kRTile;
     const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
     const uint64_t bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
     const int c = __popcll(bits);
@@ -800,7 +752,7 @@ template <typename T>
 static bool launch_average_rows_wave(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
                                      float divisor) {
     if (K < 1 || K > 4 * kRowsKB) return false;
-    const dim3 grid((unsigned)ceil_div(ceil_div(n, kRTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
+    const dim3 grid((unsigned)ceil_div(ceil_div(n, kRTile), kSpWaves)), block(64 * kSpWaves);
     if (P.ttab)
         hipLaunchKernelGGL((sparta_average_rows_wave_kernel<T, 1>), grid, block, 0, stream, P, n, (T*)src, ld, (int)K,
                            divisor);
@@ -811,23 +763,23 @@ static bool launch_average_rows_wave(hipStream_t stream, const Pred& P, int64_t 
 }
 
 // The exchange path's select on the [n, K] layout in the wave form: a
-// workgroup of GA_SP_WAVES wave tiles is exactly one count/scan tile (kSpTile),
+// workgroup of kSpWaves wave tiles is exactly one count/scan tile (kSpTile),
 // so its packed-list base comes from tile_offsets and each wave adds the
 // totals of the waves before it.  Every selected element's index goes to idx,
 // its K-replica sum (ascending replica order, the DPP lane walk) to vals.
-static_assert(GA_SP_WAVES * kWTile == kSpTile, "select wave kernel: a workgroup is one count/scan tile");
+static_assert(kSpWaves * kWTile == kSpTile, "select wave kernel: a workgroup is one count/scan tile");
 template <typename T, int KQ, int SRC>
-__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select_wave_kernel(
+__global__ __launch_bounds__(64 * kSpWaves) GA_SP_WPE_ATTR void sparta_select_wave_kernel(
     Pred P, int64_t n, const int32_t* __restrict__ tile_offsets, const T* __restrict__ src, int64_t ld, int64_t cap,
     int32_t* __restrict__ idx, T* __restrict__ vals) {
     using B = WaveBatchDpp<T, KQ>;
     __shared__ uint64_t tab[kGapTable];
-    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
-    __shared__ int wave_tot[GA_SP_WAVES];
+    __shared__ uint16_t lists[kSpWaves][kWList];
+    __shared__ int wave_tot[kSpWaves];
     if (SRC != 1) load_gap_table(P, tab);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint16_t* list = lists[wid];
-    const int64_t tile0 = ((int64_t)blockIdx.x * GA_SP_WAVES + wid) * kWTile;
+    const int64_t tile0 = ((int64_t)blockIdx.x * kSpWaves + wid) * kWTile;
     const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
     const uint64_t bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
     const int c = __popcll(bits);
@@ -873,195 +825,10 @@ __global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP_WPE_ATTR void sparta_select
     }
 }
 
-// The same select in ONE pass (no count / scan kernels, the mask drawn once):
-// each workgroup takes the next count tile by an atomic ticket (tickets follow
-// the order workgroups start, so every tile a workgroup waits on is already
-// running), draws its mask, publishes its selected count A at once, gathers its
-// first list window's K-replica sums into LDS, and only then computes its
-// output base; idx and vals are then written coalesced from LDS.
-// The base is the sum of the counts of all earlier tiles, kept in two levels
-// so that it never waits on another tile's gather: per tile a status word
-// {epoch:32, count:32} (relaxed agent-scope store; the per-launch epoch makes
-// earlier launches' words invalid, so this array is never cleared) and per
-// SUPER-tile of 64 tiles one 64-bit word {tiles done:32, count sum:32} that
-// each tile bumps with one atomic add of (1 << 32 | A) (zeroed on the stream
-// before the launch).  Wave 0 then reads up to 64 super-tile words and the
-// status words of the earlier tiles of its own super-tile per load, spinning
-// only while an earlier tile has not drawn its mask yet.  (A single-level
-// decoupled look-back either waited on its predecessors' mask draws before the
-// gather -- 0.167 ms per forced-exchange step -- or, after the gather, walked
-// back over thousands of tiles whose inclusive prefixes were not out yet --
-// 0.153 ms; the three passes take 0.108 ms, profiles/r03e_ab_sparta_select1.txt.)
-// The last ticket resets the ticket word and writes count[0] / count[1].
-// 5 waves per SIMD (96 VGPRs): the one-pass kernel keeps its look-back state
-// beside a gather batch (82 VGPRs); at 8 (64) it spilled 20-84 B per lane, at 6 (80) 12 B
-#ifndef GA_SP1_WPE
-#define GA_SP1_WPE 5
-#endif
-#define GA_SP1_WPE_ATTR __attribute__((amdgpu_waves_per_eu(GA_SP1_WPE, GA_SP1_WPE)))
-constexpr int kSuper = 64;  // tiles per super-tile
-#ifndef GA_SP1_SLEEP
-#define GA_SP1_SLEEP 8  // s_sleep units (64 clocks) between polls of a word not out yet
-#endif
-struct LookBack {
-    uint64_t* status;  // [ntiles] {epoch, count}
-    uint64_t* super;   // [ceil(ntiles / 64)] {done, sum}, zero at launch
-    uint32_t* ticket;  // zero at launch (the host clears super + ticket on the stream)
-    uint32_t epoch;    // nonzero, new per launch
-};
-
-// publish tile's count A -- one lane
-__device__ __forceinline__ void lookback_publish(const LookBack& LB, int64_t tile, int64_t A) {
-    __hip_atomic_store(LB.status + tile, ((uint64_t)LB.epoch << 32) | (uint64_t)(uint32_t)A, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(LB.super + tile / kSuper, (1ull << 32) | (uint64_t)(uint32_t)A, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// exclusive base of `tile` -- called by all 64 lanes of one wave
-__device__ __forceinline__ int64_t lookback_exclusive(const LookBack& LB, int64_t tile, int lane) {
-    const int64_t S = tile / kSuper, t0 = S * kSuper;
-    int64_t excl = 0;
-    for (int64_t s0 = 0; s0 < S; s0 += 64) {  // whole super-tiles before this one: all 64 tiles counted
-        const int64_t si = s0 + lane;
-        for (;;) {
-            const uint64_t w = si < S ? __hip_atomic_load(LB.super + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : ((uint64_t)kSuper << 32);
-            if (__ballot((w >> 32) != (uint64_t)kSuper) == 0ull) {
-                int64_t part = si < S ? (int64_t)(uint32_t)w : 0;
-#pragma unroll
-                for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
-                excl += part;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(GA_SP1_SLEEP);
-        }
-    }
-    const int64_t ti = t0 + lane;  // the earlier tiles of this super-tile
-    for (;;) {
-        const uint64_t w = ti < tile ? __hip_atomic_load(LB.status + ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : ((uint64_t)LB.epoch << 32);
-        if (__ballot((uint32_t)(w >> 32) != LB.epoch) == 0ull) {
-            int64_t part = ti < tile ? (int64_t)(uint32_t)w : 0;
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
-            return excl + part;
-        }
-        __builtin_amdgcn_s_sleep(GA_SP1_SLEEP);
-    }
-}
-
-template <typename T, int KQ, int SRC>
-__global__ __launch_bounds__(64 * GA_SP_WAVES) GA_SP1_WPE_ATTR void sparta_select1_wave_kernel(
-    Pred P, int64_t n, LookBack LB, int64_t ntiles, const T* __restrict__ src, int64_t ld, int64_t cap,
-    int32_t* __restrict__ idx, T* __restrict__ vals, int64_t* __restrict__ count) {
-    using B = WaveBatchDpp<T, KQ>;
-    __shared__ uint64_t tab[kGapTable];
-    __shared__ uint16_t lists[GA_SP_WAVES][kWList];
-    __shared__ int wave_tot[GA_SP_WAVES];
-    __shared__ float sv[GA_SP_WAVES][kWList];
-    __shared__ int64_t s_tile, s_excl;
-    if (threadIdx.x == 0) {
-        const uint32_t t = atomicAdd(LB.ticket, 1u);
-        if (t == (uint32_t)(ntiles - 1))  // every ticket of this launch is taken: ready for the next one
-            __hip_atomic_store(LB.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_tile = t;
-    }
-    if (SRC != 1) load_gap_table(P, tab);  // (its barrier also publishes s_tile)
-    else __syncthreads();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t tile = s_tile;
-    uint16_t* list = lists[wid];
-    const int64_t tile0 = (tile * GA_SP_WAVES + wid) * kWTile;
-    const int64_t e0 = tile0 + (int64_t)lane * kSpPerThread;
-    const uint64_t bits = e0 < n ? pred_bits64<SRC>(P, tab, e0, n) : 0ull;
-    const int c = __popcll(bits);
-    int x = c;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    const int total = __shfl(x, 63, 64);
-    const int local0 = x - c;
-    if (lane == 0) wave_tot[wid] = total;
-    __syncthreads();
-    int64_t A = 0;
-#pragma unroll
-    for (int w = 0; w < GA_SP_WAVES; ++w) A += wave_tot[w];
-    // the tile's aggregate goes out at once, so later tiles' look-backs can pass it
-    // while this tile is still gathering
-    if (threadIdx.x == 0) lookback_publish(LB, tile, A);
-    // window by window (one unless p is large): list + K-replica sums into LDS,
-    // then written out coalesced; the first window is gathered BEFORE the
-    // look-back, so the look-back finds its predecessors resolved
-    int64_t pos0 = 0;
-    for (int w0 = 0;; w0 += kWList) {
-        {
-            int l = local0;
-            uint64_t b = bits;
-            while (b) {
-                const int j = __builtin_ctzll(b);
-                b &= b - 1;
-                if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * kSpPerThread + j);
-                ++l;
-            }
-        }
-        wave_sync();
-        const int wtot = total - w0 < kWList ? (total - w0 > 0 ? total - w0 : 0) : kWList;
-        for (int b0 = 0; b0 < wtot; b0 += B::EB)
-            B::sums_lds(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, sv[wid]);
-        if (w0 == 0) {  // every wave of the workgroup passes here exactly once
-            if (wid == 0) {
-                const int64_t excl = lookback_exclusive(LB, tile, lane);
-                if (lane == 0) {
-                    s_excl = excl;
-                    if (tile == ntiles - 1) {
-                        count[0] = excl + A;
-                        count[1] = excl + A > cap ? 1 : 0;
-                    }
-                }
-            }
-            __syncthreads();
-            pos0 = s_excl;
-            for (int w = 0; w < wid; ++w) pos0 += wave_tot[w];
-        }
-        wave_sync();
-        for (int e = lane; e < wtot; e += 64) {  // consecutive lanes, consecutive list positions
-            const int64_t pos = pos0 + w0 + e;
-            if (pos < cap) {
-                idx[pos] = (int32_t)(tile0 + list[e]);
-                Elem<T>::store(vals + pos, sv[wid][e]);
-            }
-        }
-        if (w0 + kWList >= total) break;
-        wave_sync();  // the list and sums are rewritten by the next window
-    }
-}
-
-template <typename T>
-static bool launch_select1_wave(hipStream_t stream, const Pred& P, int64_t n, const LookBack& LB, const void* src,
-                                int64_t ld, int64_t K, int64_t cap, int32_t* idx, void* vals, int64_t* count) {
-    const int64_t ntiles = ceil_div(n, (int64_t)kSpTile);
-    const dim3 grid((unsigned)ntiles), block(64 * GA_SP_WAVES);
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, LB, ntiles, (const T*)src, ld, cap, idx, (T*)vals,
-                           count);
-    };
-    switch (K) {
-        case 4: P.ttab ? go(sparta_select1_wave_kernel<T, 1, 1>) : go(sparta_select1_wave_kernel<T, 1, 2>); return true;
-        case 8: P.ttab ? go(sparta_select1_wave_kernel<T, 2, 1>) : go(sparta_select1_wave_kernel<T, 2, 2>); return true;
-        case 16: P.ttab ? go(sparta_select1_wave_kernel<T, 4, 1>) : go(sparta_select1_wave_kernel<T, 4, 2>); return true;
-        case 32: P.ttab ? go(sparta_select1_wave_kernel<T, 8, 1>) : go(sparta_select1_wave_kernel<T, 8, 2>); return true;
-        case 64: P.ttab ? go(sparta_select1_wave_kernel<T, 16, 1>) : go(sparta_select1_wave_kernel<T, 16, 2>); return true;
-        default: return false;
-    }
-}
-
 template <typename T>
 static bool launch_select_wave(hipStream_t stream, const Pred& P, int64_t n, const int32_t* tile_offsets,
                                const void* src, int64_t ld, int64_t K, int64_t cap, int32_t* idx, void* vals) {
-    const dim3 grid((unsigned)ceil_div(n, (int64_t)kSpTile)), block(64 * GA_SP_WAVES);
+    const dim3 grid((unsigned)ceil_div(n, (int64_t)kSpTile)), block(64 * kSpWaves);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, tile_offsets, (const T*)src, ld, cap, idx, (T*)vals);
     };
@@ -1078,7 +845,7 @@ static bool launch_select_wave(hipStream_t stream, const Pred& P, int64_t n, con
 template <typename T>
 static bool launch_average_wave(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
                                 float divisor) {
-    const dim3 grid((unsigned)ceil_div(ceil_div(n, kWTile), GA_SP_WAVES)), block(64 * GA_SP_WAVES);
+    const dim3 grid((unsigned)ceil_div(ceil_div(n, kWTile), kSpWaves)), block(64 * kSpWaves);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, stream, P, n, (T*)src, ld, divisor); };
     switch (K) {
         case 4: P.ttab ? go(sparta_average_wave_kernel<T, 1, 1>) : go(sparta_average_wave_kernel<T, 1, 2>); return true;
@@ -1184,10 +951,7 @@ __global__ __launch_bounds__(kSpBlock) void sparta_pack_mask_kernel(const uint8_
 // generator offset torch hands out per bernoulli_ call.  One lane per
 // 4-element group; a workgroup stays inside one tensor (table rows: arena
 // offset, numel, first workgroup), so the lookup is a uniform binary search.
-#ifndef GA_TB_CALLS
-#define GA_TB_CALLS 4
-#endif
-constexpr int kTbCalls = GA_TB_CALLS;                 // Philox calls (4-element groups) per lane
+constexpr int kTbCalls = 4;                 // Philox calls (4-element groups) per lane
 constexpr int64_t kTbSpan = 4 * kSpBlock * kTbCalls;  // elements per workgroup
 
 // Packed output: one wavefront per workgroup span, each lane the 16 calls of
@@ -1254,53 +1018,12 @@ static Rep make_rep(int64_t ld, int layout) {
     return R;
 }
 
-// GA_SP_ROWS_WAVE=0: the tile-gather kernel for the rows layout's local average (A/B)
-static bool rows_wave_enabled() {
-    const char* e = getenv("GA_SP_ROWS_WAVE");
-    return !(e && e[0] == '0');
-}
-
-// GA_SP_SELECT1=1: the one-pass select (ticket + two-level look-back) instead of
-// the count, scan and select passes.  Opt-in: every cross-workgroup hand-off in it
-// is a memory-side round trip of several microseconds under the gather's load,
-// and the measured step is 2.7x the three passes' (0.29 vs 0.108 ms,
-// profiles/r03e_ab_sparta_select1.txt)
-static bool select1_enabled() {
-    const char* e = getenv("GA_SP_SELECT1");
-    return e && e[0] == '1';
-}
-
-// a new nonzero look-back epoch per launch, process-wide
-static uint32_t next_epoch() {
-    static std::atomic<uint32_t> g{0};
-    uint32_t e;
-    do {
-        e = g.fetch_add(1u, std::memory_order_relaxed) + 1u;
-    } while (e == 0u);
-    return e;
-}
-
 template <typename T>
 static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pred& P, int64_t cap,
                          int32_t* idx, void* vals, int64_t* count, void* work, float divisor, hipStream_t stream) {
     const int64_t ntiles = sparta_tiles(n);
     const bool v4 = R.em && K % 4 == 0 && K <= kGatherSlotsV4 && R.ei % 4 == 0 &&
                     ((uintptr_t)src % (4 * sizeof(T))) == 0;
-    if (v4 && idx && vals && count && divisor == 0.f && K >= 4 && K <= 64 && (K & (K - 1)) == 0 &&
-        select1_enabled()) {  // the exchange path's select: one pass, decoupled look-back
-        LookBack LB;
-        LB.status = (uint64_t*)((char*)work + 2 * ntiles * (int64_t)sizeof(int32_t));
-        LB.super = LB.status + ntiles;
-        const int64_t nsuper = ceil_div(ntiles, (int64_t)kSuper);
-        LB.ticket = (uint32_t*)(LB.super + nsuper);
-        LB.epoch = next_epoch();
-        if (hipMemsetAsync(LB.super, 0, nsuper * sizeof(uint64_t) + sizeof(uint32_t), stream) != hipSuccess) {
-            set_error("ga_sparta_select: ticket reset failed");
-            return GA_EHIP;
-        }
-        if (launch_select1_wave<T>(stream, P, n, LB, src, R.ei, K, cap, idx, vals, count))
-            return check_launch("ga_sparta_select(one pass)");
-    }
     int32_t* tile_offsets = nullptr;
     if (idx || vals || count) {  // positions of the packed list: count + scan passes
         int32_t* tile_counts = (int32_t*)work;
@@ -1315,14 +1038,12 @@ static int launch_select(const void* src, int64_t K, Rep R, int64_t n, const Pre
     if (v4 && !tile_offsets && !vals && divisor > 0.f && launch_average_wave<T>(stream, P, n, (void*)src, R.ei, K,
                                                                                 divisor))
         return check_launch("ga_sparta_average_local(wave)");
-    if (!R.em && !tile_offsets && !vals && divisor > 0.f && rows_wave_enabled() &&
+    if (!R.em && !tile_offsets && !vals && divisor > 0.f &&
         launch_average_rows_wave<T>(stream, P, n, (void*)src, R.ek, K, divisor))
         return check_launch("ga_sparta_average_local(rows wave)");
-#ifndef GA_SP_NO_WAVE_SELECT
     if (v4 && tile_offsets && divisor == 0.f &&
         launch_select_wave<T>(stream, P, n, tile_offsets, src, R.ei, K, cap, idx, vals))
         return check_launch("ga_sparta_select(wave)");
-#endif
     if (v4)
         hipLaunchKernelGGL((sparta_select_kernel<T, true>), dim3((unsigned)ntiles), dim3(kSpBlock), 0, stream, P, n,
                            tile_offsets, (T*)src, K, R, cap, idx, (T*)vals, divisor);
@@ -1363,11 +1084,8 @@ __global__ __launch_bounds__(kTbWordLanes) void probe_philox_kernel(int64_t nwor
 using namespace ga;
 
 extern "C" GA_API int64_t ga_sparta_workspace_bytes(int64_t n) {
-    // tile counts + tile offsets (int32 each), the one-pass select's status words (8 B
-    // per tile), super-tile words (8 B per 64 tiles) and its ticket word
-    const int64_t t = sparta_tiles(n < 0 ? 0 : n);
-    return 2 * t * (int64_t)sizeof(int32_t) + t * (int64_t)sizeof(uint64_t) +
-           ceil_div(t, (int64_t)kSuper) * (int64_t)sizeof(uint64_t) + 256;
+    // tile counts + tile offsets, one int32 each per count tile
+    return 2 * sparta_tiles(n < 0 ? 0 : n) * (int64_t)sizeof(int32_t);
 }
 
 extern "C" GA_API void ga_sparta_gap_table(double p, uint64_t* table) {

@@ -211,7 +211,7 @@ def _mptr(mask):
 
 def sparta_workspace(n, device):
     nbytes = int(lib().ga_sparta_workspace_bytes(int(n)))
-    return torch.zeros(nbytes, dtype=torch.uint8, device=device)  # the one-pass select reads its status words
+    return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)  # tile counts + offsets, written per launch
 
 
 def _sparta_set(t, layout):

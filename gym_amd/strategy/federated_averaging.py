@@ -22,12 +22,12 @@ the member rows.
 
 Sub-communicators are bounded: each costs a store barrier over the world to
 create and, under RCCL, a communicator with its own GPU buffers, and rank 0
-reshuffles every round, so up to C(K, s) member sets appear.  They are used
-only while every island of a round is cached or fits under
-MAX_ISLAND_GROUPS (and never when C(K, s) alone exceeds it, e.g. 1820 sets at
-K = 16, s = 4); otherwise the round takes the world all-gather + member-row
-mean.  The choice depends only on the broadcast permutation and the cache, so
-every rank makes the same one.
+reshuffles every round, so up to C(K, s) (+ C(K, K mod s)) member sets appear.
+They are used only when EVERY set the shuffles can produce fits under
+MAX_ISLAND_GROUPS (created lazily, as they first appear, and cached); when
+that count exceeds the cap (e.g. 1820 sets at K = 16, s = 4) no group is ever
+created and every round takes the world all-gather + member-row mean.  The
+choice depends only on K, s and the cap, so every rank makes the same one.
 """
 import math
 import random
@@ -81,14 +81,15 @@ class AveragingCommunicator(CommunicationModule):
         included).  Every island of this communication that is new gets its
         group here, on every rank, in the permutation order rank 0 broadcast:
         dist.new_group is collective over the world, so all ranks create the
-        same groups in the same order.  The group cache never exceeds
-        MAX_ISLAND_GROUPS (module docstring)."""
+        same groups in the same order.  Sub-communicators are used only when
+        every possible island set fits under MAX_ISLAND_GROUPS (module
+        docstring)."""
         if self._groups_possible(num_nodes) > MAX_ISLAND_GROUPS:
             return False, None
         keys = [tuple(sorted(i)) for i in self._islands]
         new = [k for k in dict.fromkeys(keys) if len(k) > 1 and k not in self._groups]
-        if len(self._groups) + len(new) > MAX_ISLAND_GROUPS:
-            return False, None
+        # every possible set fits under the cap (checked above), so the cache cannot outgrow it
+        assert len(self._groups) + len(new) <= MAX_ISLAND_GROUPS
         me = dist.get_rank()
         for key in new:
             g = dist.new_group(list(key))

@@ -134,6 +134,12 @@ def draw_masks(selector, params, views, skip, iteration, state, bits=None, coll=
                 v.bernoulli_(state.pfull[i])
 
     on_gpu = _on_gpu(params)
+    if on_gpu and MaskDraw.fused and coll is not None and coll.exchange and _capturing():
+        # the fused and the torch draws exchange different things (16 B of generator state vs the
+        # packed masks), and the choice is agreed across ranks by a collective: a rank inside a
+        # graph capture would take the torch path alone and the ranks' collectives would not match
+        raise RuntimeError("SPARTA: a multi-rank mask draw cannot run inside a graph capture (the ranks "
+                           "must agree on the draw path); capture the single-process step only")
     # inside a user's graph capture the generator offsets are graph-relative: torch's own kernels then
     if (on_gpu and MaskDraw.fused and not _capturing()
             and fused_draw_matches_torch(params[0].device, coll)):

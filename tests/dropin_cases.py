@@ -143,4 +143,7 @@ def check(z, name, states, log, exact=False):
         want = z[f"{name}_val_{kind}"]
         got = np.array(evals.get(kind, []))
         assert len(got) == len(want), (name, kind, got, want)
-        np.testing.assert_allclose(got, want, rtol=2e-4 if not demo else 2e-3, atol=1e-6)
+        if exact:
+            assert np.array_equal(got.astype(np.float64), want), (name, kind, got, want)
+        else:
+            np.testing.assert_allclose(got, want, rtol=2e-4 if not demo else 2e-3, atol=1e-6)

@@ -1025,112 +1025,45 @@ def test_fused_draw_self_check():
     assert torch.equal(torch.cuda.get_rng_state(), before)
 
 
-@pytest.mark.parametrize("K,zero_chunks", [(1, False), (3, True)])
-def test_demo_encode_loader_consumer_matches_all_in_one(monkeypatch, K, zero_chunks):
-    """ga_demo_encode_sym's loader/consumer kernel (opt-in, GA_DEMO_ENCODE_LC=1)
-    against its all-in-one kernel (the default, GA_DEMO_ENCODE_LC=0): the same
-    arithmetic per chunk, so payload, residual delta and weight-decayed params
-    are bit-identical -- over every GPT-2-like chunk kind, batched replicas,
-    and all-zero chunks (the > kCand top-k fallback)."""
-    from gym_amd import ops
-    shapes = [(192, 128), (768,), (64, 64), (128, 192), (320,), (64, 256), (1024, 64)]
-    L, plan, a = _demo_setup(shapes, K, seed=11 + K)
-    assert plan.wave_encode
-    if zero_chunks:  # tensor 0's second 64-row block and tensor 6's first chunk: delta = grad = 0
-        for k in range(K):
-            for arr in (a["g"], a["d"]):
-                v = arr[k, L.offsets[0]:L.offsets[0] + L.numels[0]].reshape(192, 128)
-                v[64:128] = 0
-                v2 = arr[k, L.offsets[6]:L.offsets[6] + L.numels[6]].reshape(1024, 64)
-                v2[:64] = 0
-    lr, decay, wdf = 0.01, 0.999, float(np.float32(1.0 - 0.01 * 0.1))
-    out = {}
-    for lc in ("0", "1"):
-        monkeypatch.setenv("GA_DEMO_ENCODE_LC", lc)
-        P, G, D = t(a["p"]), t(a["g"]), t(a["d"])
-        payload = torch.zeros(K, 2 * plan.M, dtype=torch.int32, device=DEV)
-        ops.demo_encode(plan, P, G, D, payload, lr, decay, wdf)
-        out[lc] = (host(P), host(D), payload.cpu().numpy())
-    for a0, a1, what in zip(out["0"], out["1"], ("p", "delta", "payload")):
-        assert np.array_equal(a0, a1), what
-
-
-@pytest.mark.parametrize("S,K,with_grad", [(1, 1, True), (4, 1, False), (8, 3, True)])
-def test_demo_decode_consumer_updater_matches_one_wave(monkeypatch, S, K, with_grad):
-    """ga_demo_decode_sym's consumer/updater kernel (opt-in, GA_DEMO_DECODE_LC=1,
-    64x64 chunks at S <= 8 sources) against its one-wave-per-chunk kernel (the
-    default, GA_DEMO_DECODE_LC=0): the same per-chunk arithmetic, so params and signs
-    are bit-identical -- S sources with colliding indices, batched replicas,
-    with and without the grad output."""
-    from gym_amd import ops
-    shapes = [(192, 128), (768,), (64, 64), (128, 192), (320,), (64, 256), (1024, 64)]
-    L, plan, a = _demo_setup(shapes, S, seed=40 + S)
-    assert plan.wave_encode
-    P, G, D = t(a["p"]), t(a["g"]), t(a["d"])
-    payload = torch.zeros(S, 2 * plan.M, dtype=torch.int32, device=DEV)
-    ops.demo_encode(plan, P, G, D, payload, 0.01, 0.999, 1.0)  # S sources' payloads
-    if S > 1:  # force collisions: source 1 repeats source 0's indices
-        payload[1, : plan.M] = payload[0, : plan.M]
-    P0 = torch.from_numpy(np.repeat(a["p"][:1], K, axis=0)).to(DEV)
-    out = {}
-    for lc in ("0", "1"):
-        monkeypatch.setenv("GA_DEMO_DECODE_LC", lc)
-        Pk = P0.clone()
-        Gk = torch.zeros_like(Pk) if with_grad else None
-        ops.demo_decode(plan, payload, Pk, Gk, 0.01)
-        out[lc] = (host(Pk), host(Gk) if with_grad else None)
-    assert np.array_equal(out["0"][0], out["1"][0])
-    if with_grad:
-        assert np.array_equal(out["0"][1], out["1"][1])
-        assert np.isin(out["1"][1], (-1.0, 0.0, 1.0)).all()
-
-
 @pytest.mark.parametrize("K,n,p,src_kind", [(32, 1_000_003, 0.005, "philox"), (4, 3 * 16384 + 77, 0.3, "philox"),
                                             (8, 2_000_000, 0.01, "torch"), (64, 16384 * 5, 0.6, "bits")])
-def test_sparta_one_pass_select_matches_three_pass(monkeypatch, K, n, p, src_kind):
-    """The exchange path's select on an element-major set in ONE pass (ticket
-    + decoupled look-back) against the count -> scan ->
-    select passes (GA_SP_SELECT1=0) and the oracle: the same packed index list,
-    the same K-replica sums, the same count -- launched repeatedly on one
-    workspace (each launch's look-back epoch must ignore the last one's status
-    words), with a cap that overflows on the last launch."""
+def test_sparta_select_repeated_launches_overflow(K, n, p, src_kind):
+    """The exchange path's select on an element-major set (count -> scan ->
+    select) against the oracle, launched repeatedly on one workspace: the same
+    packed index list, the same K-replica sums and count every launch, with a
+    cap that overflows on the last launch (count[1] set, the list truncated)."""
     from gym_amd import ops
     rng = np.random.default_rng(K + n)
     x = rng.standard_normal((n, K)).astype(np.float32)  # [n, K] element-major
     src = t(x)
     seed = 0xABCDEF
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("GA_SP_SELECT1", mode)
-        for it in range(3):
-            if src_kind == "philox":
-                m = osparta.philox_mask(n, seed, it, p)
-                kw = dict(seed=seed, iteration=it, p=p)
-            elif src_kind == "bits":
-                m = rng.random(n) < p if mode == "0" else out[("0", it)][3]
-                bits = torch.from_numpy(osparta.pack_mask(m).view(np.int64)).to(DEV)
-                kw = dict(mask=bits)
-            else:  # the in-kernel reference draw (GA_MASK_TORCH)
-                L = __import__("gym_amd.arena", fromlist=["ArenaLayout"]).ArenaLayout([(n,)])
-                table, nb = ops.sparta_bernoulli_table(L.offsets, L.numels, DEV)
-                m = osparta.torch_gpu_bernoulli(n, p, 1234, 12 * it)
-                kw = dict(mask=ops.TorchDraw(table, p, 1234, 12 * it, 12))
-            want = np.flatnonzero(m)
-            cap = len(want) + 16 if it < 2 else max(1, len(want) - 5)  # the last launch overflows
-            idx, count, work = (out[("ws", mode)] if ("ws", mode) in out else _sparta_buffers(n, len(want) + 4096))
-            out[("ws", mode)] = (idx, count, work)
-            vals = torch.empty(cap, device=DEV)
-            ops.sparta_select(src, n, cap, idx, vals, count, work, layout="elem", **kw)
-            c = host(count).astype(np.int64)
-            assert c[0] == len(want) and c[1] == int(len(want) > cap), (mode, it, c, len(want))
-            k = min(cap, len(want))
-            assert np.array_equal(idx.cpu().numpy()[:k], want[:k]), (mode, it)
-            sums = oreduce.mean_reduce(list(x[want[:k]].T), divisor=1)
-            assert np.array_equal(host(vals)[:k], sums), (mode, it)
-            out[(mode, it)] = (idx.cpu().numpy()[:k].copy(), host(vals)[:k].copy(), c, m)
+    ws = None
     for it in range(3):
-        for a, b in zip(out[("0", it)][:3], out[("1", it)][:3]):
-            assert np.array_equal(a, b)
+        if src_kind == "philox":
+            m = osparta.philox_mask(n, seed, it, p)
+            kw = dict(seed=seed, iteration=it, p=p)
+        elif src_kind == "bits":
+            m = rng.random(n) < p
+            bits = torch.from_numpy(osparta.pack_mask(m).view(np.int64)).to(DEV)
+            kw = dict(mask=bits)
+        else:  # the in-kernel reference draw (GA_MASK_TORCH)
+            L = __import__("gym_amd.arena", fromlist=["ArenaLayout"]).ArenaLayout([(n,)])
+            table, nb = ops.sparta_bernoulli_table(L.offsets, L.numels, DEV)
+            m = osparta.torch_gpu_bernoulli(n, p, 1234, 12 * it)
+            kw = dict(mask=ops.TorchDraw(table, p, 1234, 12 * it, 12))
+        want = np.flatnonzero(m)
+        cap = len(want) + 16 if it < 2 else max(1, len(want) - 5)  # the last launch overflows
+        if ws is None:
+            ws = _sparta_buffers(n, len(want) + 4096)
+        idx, count, work = ws
+        vals = torch.empty(cap, device=DEV)
+        ops.sparta_select(src, n, cap, idx, vals, count, work, layout="elem", **kw)
+        c = host(count).astype(np.int64)
+        assert c[0] == len(want) and c[1] == int(len(want) > cap), (it, c, len(want))
+        k = min(cap, len(want))
+        assert np.array_equal(idx.cpu().numpy()[:k], want[:k]), it
+        sums = oreduce.mean_reduce(list(x[want[:k]].T), divisor=1)
+        assert np.array_equal(host(vals)[:k], sums), it
 
 
 @pytest.mark.parametrize("K,n,p,src_kind,dtype", [(32, 1_000_003, 0.005, "philox", "f32"),
@@ -1139,12 +1072,11 @@ def test_sparta_one_pass_select_matches_three_pass(monkeypatch, K, n, p, src_kin
                                                   (128, 4096 * 9, 0.9, "bits", "f32"),
                                                   (8, 2_000_000, 0.01, "torch", "f32"),
                                                   (1, 70_001, 0.05, "philox", "f32")])
-def test_sparta_rows_wave_matches_tile_gather(monkeypatch, K, n, p, src_kind, dtype):
-    """The replica loop's [K, ld] rows local average in the wave form (one lane
-    per listed element, every replica's word in flight; GA_SP_ROWS_WAVE) against
-    the tile-gather kernel (GA_SP_ROWS_WAVE=0) and the oracle: bit-identical
-    replicas, dense tiles (several list windows, more than 64 elements per
-    batch), K > 32 (several load batches), bf16, each mask source."""
+def test_sparta_rows_local_average(K, n, p, src_kind, dtype):
+    """The replica loop's [K, ld] rows local average (the wave form: one lane
+    per listed element, every replica's word in flight) against the oracle:
+    bit-identical replicas, dense tiles (several list windows, more than 64
+    elements per batch), K > 32 (several load batches), bf16, each mask source."""
     from gym_amd import ops
     rng = np.random.default_rng(K + n)
     ld = n + 61
@@ -1162,13 +1094,9 @@ def test_sparta_rows_wave_matches_tile_gather(monkeypatch, K, n, p, src_kind, dt
         table, _ = ops.sparta_bernoulli_table(L.offsets, L.numels, DEV)
         m = osparta.torch_gpu_bernoulli(n, p, 1234, 24)
         kw = dict(mask=ops.TorchDraw(table, p, 1234, 24, 12))
-    got = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("GA_SP_ROWS_WAVE", mode)
-        src = torch.from_numpy(x).to(DEV).to(tdt)
-        ops.sparta_average_local(src, n, float(K), layout="rows", **kw)
-        got[mode] = src.float().cpu().numpy()
-    assert np.array_equal(got["0"], got["1"])
+    src = torch.from_numpy(x).to(DEV).to(tdt)
+    ops.sparta_average_local(src, n, float(K), layout="rows", **kw)
+    got = {"1": src.float().cpu().numpy()}
     if dtype == "f32":
         want = osparta.sparse_average(list(x[:, :n]), m)
         for k in range(K):

@@ -25,9 +25,11 @@ CASES = [
     ("fedavg", 2, {}), ("fedavg", 3, {"island_size": 2}), ("fedavg", 4, {"island_size": 2}),
     ("fedavg", 4, {"island_size": 3}),
     # many rounds: C(4, 2) = 6 sets > 2 -> world all-gather every round, no group created;
-    # C(5, 2) + remainder at a cap of 8: groups until the cache is full, then the world path
+    # C(5, 2) = 10 sets <= 12: every round on cached sub-communicators (created as they appear);
+    # C(5, 2) = 10 sets > 8: the world all-gather every round
     ("fedavg", 4, {"island_size": 2, "rounds": 12, "max_groups": 2}),
     ("fedavg", 5, {"island_size": 2, "rounds": 12, "max_groups": 12}),
+    ("fedavg", 5, {"island_size": 2, "rounds": 6, "max_groups": 8}),
     ("demo", 2, {}), ("demo_pipe", 2, {}), ("demo_pipe", 3, {"pieces": 2}),
 ]
 
