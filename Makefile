@@ -10,7 +10,7 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -fvisibility=hidden -Wal
 .PHONY: all clean oracle asan variant
 all: $(LIB)
 
-build/%.o: gym_amd/csrc/%.hip gym_amd/csrc/ga_common.h include/gym_amd.h
+build/%.o: gym_amd/csrc/%.hip gym_amd/csrc/ga_common.h gym_amd/csrc/adam_math.h include/gym_amd.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -356,7 +356,9 @@ def bench_diloco(args, coll, dev):
                           "copy_GBps": round(copy_sus, 1),
                           "frac_of_copy": round(alg_bytes / (sus_ms * 1e-3) / 1e9 / copy_sus, 4)} if sus_ms else None,
             "copy_GBps": round(copy, 1) if copy else None,
-            "frac_of_copy": round(achieved / copy, 4) if copy else None},
+            "frac_of_copy": round(achieved / copy, 4) if copy else None,
+            # master/momentum placement chosen by DiLoCoOuter._place (probe times per candidate)
+            "placement": eng.placement},
     }
     if coll.exchange:
         # the exchange alone: reduce-scatter + all-gather of the whole arena (the bytes of one

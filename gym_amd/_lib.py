@@ -59,6 +59,7 @@ SIGNATURES = {
     "ga_probe_random_words": (c_i32, [c_p, c_i64, c_i64, c_p, c_i64, c_i32, c_p]),
     "ga_probe_philox": (c_i32, [c_i64, c_p, c_p]),
     "ga_probe_chunk_stream": (c_i32, [c_p, c_p, c_i64, c_i64, c_i32, c_p]),
+    "ga_probe_diloco_placement": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "ga_replica_mean": (c_i32, [c_i32, c_p, c_i64, c_i64, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_p]),
     "ga_diloco_outer": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_i32, c_i32, c_f32, c_f32,
                                 c_f32, c_f32, c_i32, c_p, c_i64, c_i64, c_p]),
@@ -86,6 +87,9 @@ SIGNATURES = {
     "ga_grad_clip_coef": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "ga_adam_step": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                              c_f32, c_f32, c_f32, c_p, c_p]),
+    "ga_adam_sparta_step": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32,
+                                    c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_i32, c_u64, c_u64, c_f64, c_p, c_i64,
+                                    c_f32, c_p]),
 }
 
 _lib = None

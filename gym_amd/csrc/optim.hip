@@ -13,6 +13,7 @@
 // 28 bytes per element (read p, g, m, v; write p, m, v), +4 when the clipped
 // gradient is written back.
 #include "ga_common.h"
+#include "adam_math.h"
 
 
 namespace ga {
@@ -20,25 +21,6 @@ namespace ga {
 constexpr int kOptBlock = 256;
 constexpr int64_t kOptChunk = 1024;  // float4 vectors per workgroup
 constexpr int kSumsqBlocks = 1024;   // partials of the norm reduction
-
-struct AdamParams {
-    float lerp_w, b2, one_m_b2, eps, wd_factor, l2_wd, step_size, bc2_sqrt;
-};
-
-__device__ __forceinline__ float lerp_torch(float a, float b, float w) {
-    // ATen lerp: weight < 0.5 ? a + w*(b-a) : b - (b-a)*(1-w)
-    const float d = b - a;
-    return w < 0.5f ? fmaf(w, d, a) : fmaf(-d, 1.f - w, b);
-}
-
-__device__ __forceinline__ void adam_elem(float& p, float& g, float& m, float& v, const AdamParams& ap) {
-    if (ap.wd_factor != 1.f) p = p * ap.wd_factor;  // AdamW
-    if (ap.l2_wd != 0.f) g = fmaf(ap.l2_wd, p, g);   // Adam
-    m = lerp_torch(m, g, ap.lerp_w);
-    v = fmaf(ap.one_m_b2 * g, g, v * ap.b2);
-    const float denom = sqrtf(v) / ap.bc2_sqrt + ap.eps;
-    p = fmaf(ap.step_size, m / denom, p);
-}
 
 __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ param, float* __restrict__ grad,
                                                          float* __restrict__ m_, float* __restrict__ v_, int64_t n,

@@ -144,6 +144,33 @@ __global__ __launch_bounds__(kBlock) void diloco_outer_kernel(
     }
 }
 
+// Placement probe of the fused outer step (no reference counterpart): the exact
+// access pattern of diloco_outer_kernel<float, float, true> -- workgroup b's block
+// of K replica streams, master and momentum read, the same blocks written through
+// the same stores -- with every value written back unchanged, so a caller can time
+// candidate master/momentum buffers against a live replica set without side
+// effects.  K <= kProbeK (the replicas are held in registers to be written back).
+constexpr int kProbeK = 16;
+__global__ __launch_bounds__(kBlock) void diloco_probe_kernel(float* src, int64_t K, int64_t ld_src, int64_t n,
+                                                              float* master, float* mom) {
+    int64_t lo, hi;
+    chunk_range(n >> 2, lo, hi);
+    for (int64_t v = lo + threadIdx.x; v < hi; v += kBlock) {
+        float4 x[kProbeK];
+#pragma unroll
+        for (int k = 0; k < kProbeK; ++k)
+            if (k < K) x[k] = stream_load(reinterpret_cast<const float4*>(src + k * ld_src) + v);
+        const float4 m = stream_load(reinterpret_cast<const float4*>(master) + v);
+        const float4 b = stream_load(reinterpret_cast<const float4*>(mom) + v);
+        const uint32_t i = (uint32_t)(v - lo);
+        store_sc1(reinterpret_cast<float4*>(master) + lo, i, m);
+        store_sc1(reinterpret_cast<float4*>(mom) + lo, i, b);
+#pragma unroll
+        for (int k = 0; k < kProbeK; ++k)
+            if (k < K) store_sc1(reinterpret_cast<float4*>(src + k * ld_src) + lo, i, x[k]);
+    }
+}
+
 static bool aligned(const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; }
 
 template <typename T>
@@ -249,4 +276,18 @@ extern "C" GA_API int ga_diloco_outer(int dtype, const void* src, int64_t K, int
             set_error("ga_diloco_outer: unknown dtype %d", dtype);
             return GA_EINVAL;
     }
+}
+
+extern "C" GA_API int ga_probe_diloco_placement(float* src, int64_t K, int64_t ld_src, int64_t n, float* master,
+                                                float* mom, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(n >= 0 && n % 4 == 0 && K >= 1 && K <= kProbeK, "ga_probe_diloco_placement: bad sizes n=%lld K=%lld "
+               "(n a multiple of 4, K <= %d)", (long long)n, (long long)K, kProbeK);
+    if (n == 0) return GA_OK;
+    GA_REQUIRE(src && master && mom, "ga_probe_diloco_placement: null buffer");
+    GA_REQUIRE(K == 1 || (ld_src >= n && ld_src % 4 == 0), "ga_probe_diloco_placement: bad ld_src");
+    GA_REQUIRE(aligned(src, 16) && aligned(master, 16) && aligned(mom, 16), "ga_probe_diloco_placement: alignment");
+    hipLaunchKernelGGL(diloco_probe_kernel, dim3(chunk_grid(n / 4)), dim3(kBlock), 0, stream, src, K, ld_src, n,
+                       master, mom);
+    return check_launch("ga_probe_diloco_placement");
 }

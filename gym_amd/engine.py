@@ -165,6 +165,10 @@ class MeanReduce:
             ops.replica_mean(self.sum, reps, n=n, divisor=self.K_total)
 
 
+# master+momentum buffers timed against the replica set before the first outer step
+PLACEMENT_CANDIDATES = 6
+
+
 class DiLoCoOuter:
     """Fused DiLoCo outer step.  With RCCL and world > 1 the master copy and
     the momentum are sharded: chunked reduce-scatter(sum) -> fused update of
@@ -187,8 +191,12 @@ class DiLoCoOuter:
         else:
             self.plan = None
             self.per = self.n
-        self.master = torch.zeros(self.per, device=device, dtype=torch.float32)
-        self.mom = torch.zeros(self.per, device=device, dtype=torch.float32) if momentum != 0 else None
+        # master and momentum in one allocation (a placement candidate, see _place)
+        self._state = torch.zeros((2 if momentum != 0 else 1) * self.per, device=device, dtype=torch.float32)
+        self.master = self._state[:self.per]
+        self.mom = self._state[self.per:] if momentum != 0 else None
+        self.placement = None  # the placement probe's record (bench / DESIGN)
+        self._placed_for = None
         self.first = True
         self.dtype = dtype
         self.sum = torch.empty(n, device=device, dtype=dtype) if (X and not self.shard) else None
@@ -214,10 +222,58 @@ class DiLoCoOuter:
     def _outer_shard(self, rs_shard, m, own):
         self._outer(rs_shard, self.K_total, own, m[0], m[1])
 
+    def _place(self, reps):
+        """Choose where master / momentum live, once per replica set.
+
+        On MI355X the fused step's rate depends on the PHYSICAL placement of
+        its 2K + 4 streams: with the replica set fixed, master/momentum buffers
+        at different physical addresses run the GPT-2 124M x 8 step at 1.65 ms
+        or 1.88 ms, and the same virtual layout lands in either mode from one
+        process to the next (tools/ubench_diloco_layout.cpp,
+        profiles/r04b_placement_search.txt, r04c_placement_sweep.txt) -- the
+        between-process spread of rounds 1-3.  So PLACEMENT_CANDIDATES
+        separately allocated master+momentum buffers are timed once against the
+        live replica set with ga_probe_diloco_placement (the step's exact access
+        pattern, every value written back unchanged: ~2 ms per launch, three
+        launches per candidate) and the fastest is kept; the state is copied
+        into it and the others are freed."""
+        key = (reps.data_ptr(), reps.stride(0))
+        if self._placed_for == key:
+            return
+        self._placed_for = key
+        per = self.per
+        if (self.coll.exchange or reps.device.type != "cuda" or reps.dtype != torch.float32 or self.mom is None
+                or reps.shape[0] > 16 or 4 * per < SHARD_MIN_BYTES or PLACEMENT_CANDIDATES < 2
+                or reps.stride(1) != 1 or reps.stride(0) % 4 or per % 4):
+            return
+        cands = [self._state] + [torch.empty(2 * per, device=reps.device, dtype=torch.float32)
+                                 for _ in range(PLACEMENT_CANDIDATES - 1)]
+        src = reps[:, :per]
+        times = []
+        for c in cands:
+            ops.probe_diloco_placement(src, per, c[:per], c[per:])  # warm-up
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                ops.probe_diloco_placement(src, per, c[:per], c[per:])
+            e1.record()
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) / 3)
+        best = min(range(len(cands)), key=lambda i: times[i])
+        if best != 0:
+            cands[best].copy_(self._state)
+            self._state = cands[best]
+            self.master, self.mom = self._state[:per], self._state[per:]
+        del cands, src
+        torch.cuda.empty_cache()  # the losing candidates go back to the driver
+        self.placement = {"candidates": PLACEMENT_CANDIDATES, "probe_ms": [round(t, 4) for t in times],
+                          "chosen": best}
+
     def __call__(self, reps):
         n = self.n
         self.launch_elems = []
         if not self.coll.exchange:  # one kernel: read every replica, update, write every replica
+            self._place(reps)
             self._outer(reps[:, :n], self.K_total, reps[:, :n])
         elif not self.shard:  # gloo: all-reduce the sum, replicated update
             ops.replica_mean(reps, self.sum, n=n, divisor=1.0)

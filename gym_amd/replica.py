@@ -169,14 +169,25 @@ class ReplicaRunner:
             if s.local_step % s.H == 0 and s.local_step > 0:
                 self.outer(P)
         elif isinstance(s, SPARTAStrategy):
-            self._inner()
-            if self.philox:
-                self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
+            if self._fused_sparta():
+                # inner AdamW and the sparse average in one pass (ga_adam_sparta_step): the
+                # masks are drawn first -- the optimizer consumes no random numbers, so the
+                # generator ends where the reference's optim.step() + communicate leave it
+                if self.philox:
+                    kw = dict(seed=self.seed, iteration=self.iteration, p=s.index_selector.p,
+                              skip=self._skip_table())
+                else:
+                    kw = dict(mask=self._build_mask())
+                self.optim.step(max_norm=self.max_norm or None, sparta=dict(divisor=float(self.num_nodes), **kw))
             else:
-                sel = s.index_selector
-                m = self._build_mask()
-                self.sparta(P, mask=m, mask_cap=self.sparta.cap if type(sel) is RandomIndexSelector else None,
-                            mask_shared=self.mask_shared)
+                self._inner()
+                if self.philox:
+                    self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
+                else:
+                    sel = s.index_selector
+                    m = self._build_mask()
+                    self.sparta(P, mask=m, mask_cap=self.sparta.cap if type(sel) is RandomIndexSelector else None,
+                                mask_shared=self.mask_shared)
             self.iteration += 1
         elif isinstance(s, FedAvgStrategy):
             self._inner()
@@ -188,6 +199,14 @@ class ReplicaRunner:
             for cb in s.lr_callbacks:
                 cb(self.lr_scheds[0].get_last_lr()[0])
         s.local_step += 1
+
+    # the single-process SPARTA step fused into the inner AdamW launch (tests turn it off to
+    # compare against the two-launch path)
+    fuse_sparta = True
+
+    def _fused_sparta(self):
+        return (self.fuse_sparta and isinstance(self.optim, ArenaAdam) and not self.coll.exchange
+                and self.ra.dtype == torch.float32 and self.ra.ld % 4 == 0)
 
     def _grad_less(self):
         """Indices of node 0's tensors without a gradient (skipped, sparta.py:29-30)."""

@@ -131,11 +131,47 @@ static int search(int seed, int ncand, int reps, hipStream_t s) {
     return 0;
 }
 
+// sweep mode: one 60 GiB pool; (a) replicas packed at 0, master + momentum adjacent at
+// 1 GiB steps from 4 to 52 GiB; (b) replicas packed at 16 / 32 GiB with master +
+// momentum at 0; (c) replica rows spread S GiB apart with master + momentum after them
+static int sweep(int reps, hipStream_t s) {
+    const int64_t G1 = 1LL << 30;
+    const int64_t pool_bytes = 60 * G1;
+    char* pool;
+    CK(hipMalloc(&pool, pool_bytes));
+    CK(hipMemset(pool, 0, pool_bytes));
+    const double alg = (2.0 * K + 4.0) * 4.0 * N;
+    auto time2 = [&](const Layout& L) { const float a = run(L, reps, s), b = run(L, reps, s); return a < b ? a : b; };
+    auto at = [&](int64_t off) { return (float*)(pool + off); };
+    const int64_t one_b = 4 * N;
+    for (int64_t g = 4; g <= 52; ++g) {
+        const Layout L{"a", at(0), N, at(g * G1), at(g * G1 + one_b)};
+        const float t = time2(L);
+        printf("a replicas@0 master@%lldG mom adjacent: %.4f ms frac %.3f\n", (long long)g, t, alg / t / 1e6 / 8000.0);
+    }
+    for (int64_t r : {16LL, 32LL, 48LL}) {
+        const Layout L{"b", at(r * G1), N, at(0), at(one_b)};
+        const float t = time2(L);
+        printf("b replicas@%lldG master@0 mom adjacent: %.4f ms frac %.3f\n", (long long)r, t, alg / t / 1e6 / 8000.0);
+    }
+    for (int64_t S : {1LL, 2LL, 4LL, 6LL}) {
+        const int64_t ld = S * G1 / 4;
+        const Layout L{"c", at(0), ld, at(K * S * G1), at(K * S * G1 + one_b)};
+        if (K * S * G1 + 2 * one_b > pool_bytes) continue;
+        const float t = time2(L);
+        printf("c rows %lldG apart, master@%lldG: %.4f ms frac %.3f\n", (long long)S, (long long)(K * S), t,
+               alg / t / 1e6 / 8000.0);
+    }
+    fflush(stdout);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 4;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (argc > 3 && !strcmp(argv[3], "sweep")) return sweep(reps, s);
     if (argc > 3 && !strcmp(argv[3], "search")) return search(argc > 4 ? atoi(argv[4]) : 0, argc > 5 ? atoi(argv[5]) : 40, reps, s);
     std::vector<Layout> Ls;
     // (a) the product's allocation: replica set, master, momentum as separate allocations
