@@ -518,6 +518,42 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
     return out
 
 
+def bench_sparta_replica_step(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
+    """configs[3] as the replica training loop runs it (gym_amd.replica, one GPU):
+    the inner AdamW over the 32 nodes' [K, ld] rows (ga_adam_step) followed by
+    SPARTA's sparse average with the reference's torch.bernoulli draw in-kernel
+    (ga_sparta_average_local, rows layout; communicate_optimize_strategy.py:67-85).
+    added_ms = what the SPARTA average adds to the AdamW pass.  (A fused
+    element-major AdamW + average pass measured no faster: the element-major
+    traversal of 32 rows costs ~0.9 ms over the replica-major AdamW,
+    profiles/r04f_ubench_adam_sparta.txt.)"""
+    if coll.world > 1:
+        return {"skipped": "single-GPU replica loop (no exchange)"}
+    shapes = MODELS[model]()
+    layout = ArenaLayout(shapes)
+    ld = layout.n
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    P = torch.randn(K, ld, device=dev, generator=g).mul_(0.02)
+    G = torch.randn(K, ld, device=dev, generator=g).mul_(1e-3)
+    M, V = torch.zeros_like(P), torch.zeros_like(P)
+    table, _ = ops.sparta_bernoulli_table(layout.offsets, layout.numels, dev)
+    draw = ops.TorchDraw(table, p, 42, 0, 12)
+    hp = dict(lerp_w=0.1, beta2=0.999, one_m_beta2=1 - 0.999, eps=1e-8, wd_factor=1 - 1e-3 * 0.01, l2_wd=0.0,
+              step_size=-1e-3 / 0.1, bc2_sqrt=(1 - 0.999) ** 0.5)
+    reps = max(5, args.steps // 2)
+    adam = queued_ms(lambda: ops.adam_step(P, G, M, V, **hp), reps, dev)
+    step = queued_ms(lambda: (ops.adam_step(P, G, M, V, **hp),
+                              ops.sparta_average_local(P, ld, float(K), mask=draw, layout="rows")), reps, dev)
+    alg = 28 * K * ld  # read p, g, m, v; write p, m, v
+    del P, G, M, V
+    return {"model": model, "K": K, "p": p, "mask": "the reference's torch.bernoulli draw, in-kernel",
+            "adamw_alone_ms": round(adam, 4), "adamw_then_sparta_ms": round(step, 4),
+            "added_ms": round(step - adam, 4),
+            "adamw_alg_GBps": round(alg / (adam * 1e-3) / 1e9, 1),
+            "adamw_frac_hbm": round(alg / (adam * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def bench_simple(args, coll, dev, K_total=8, model="gpt2-char"):
     """configs[1]: 8 char-level nodes, on one GPU or one per GPU (8/G per GPU)."""
     K = max(1, K_total // coll.world)
@@ -787,6 +823,7 @@ def main():
                   ("sparta_k32_rows_torch_mask",  # the replica training loop's own step: rows + the reference draw
                    lambda a, c, d: bench_sparta(a, c, d, layout_kind="rows", mask_source="torch")),
                   ("sparta_k32_torch_mask", lambda a, c, d: bench_sparta(a, c, d, mask_source="torch")),
+                  ("sparta_k32_replica_step", bench_sparta_replica_step),
                   ("simple_reduce_char_k8", bench_simple),
                   ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
     if args.only and args.only != "diloco":

@@ -87,9 +87,6 @@ SIGNATURES = {
     "ga_grad_clip_coef": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "ga_adam_step": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                              c_f32, c_f32, c_f32, c_p, c_p]),
-    "ga_adam_sparta_step": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32,
-                                    c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_i32, c_u64, c_u64, c_f64, c_p, c_i64,
-                                    c_f32, c_p]),
 }
 
 _lib = None

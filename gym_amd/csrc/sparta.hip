@@ -24,7 +24,6 @@
 
 
 #include "ga_common.h"
-#include "adam_math.h"
 
 namespace ga {
 
@@ -768,126 +767,6 @@ static bool launch_average_rows_wave(hipStream_t stream, const Pred& P, int64_t 
 // so its packed-list base comes from tile_offsets and each wave adds the
 // totals of the waves before it.  Every selected element's index goes to idx,
 // its K-replica sum (ascending replica order, the DPP lane walk) to vals.
-// ---- the replica loop's inner AdamW + SPARTA average in ONE pass ------------
-// CommunicateOptimizeStrategy.step (communicate_optimize_strategy.py:67-85) runs
-// the inner optimizer and then SparseCommunicator.communicate (sparta.py:24-44).
-// On a [K, ld] replica set of one process (every node local, no exchange) both
-// are one streaming pass: a lane owns one 4-element vector of every replica,
-// runs Adam on replica 0, 1, ..., K-1 (the bits of adam_kernel), keeps the
-// ascending-replica fp32 sum of the new parameters, and where the vector holds
-// selected elements writes sum / divisor into every replica's word -- the sum
-// and division of ga_sparta_average_local's rows kernel, so the result is
-// bit-identical to ga_adam_step followed by ga_sparta_average_local, without
-// that kernel's random 4-B word reads (the sum comes from the Adam pass) and
-// with its word writes landing on lines this workgroup has just stored (p is
-// stored with the plain policy, which keeps the line in the XCD's L2).
-// Mask: the reference draw (GA_MASK_TORCH) as ONE Philox4x32-10 call per lane
-// -- torch's 4-element group is exactly the lane's vector; other sources: the
-// 64-element word of the lane's group, drawn once per 16 lanes.
-
-// The 4 elements at e0 (e0 % 4 == 0) as ga_sparta_torch_bernoulli draws them
-__device__ __forceinline__ uint32_t torch_bits4(const Pred& P, int64_t e0) {
-    const int64_t ef = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(e0 >> 32)) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)e0));
-    int lo = 0, hi = P.tn - 1;
-    while (lo < hi) {  // wave-uniform search for the first lane's tensor, then walk forward
-        const int mid = (lo + hi + 1) >> 1;
-        if (P.ttab[3 * mid] <= ef) lo = mid;
-        else hi = mid - 1;
-    }
-    while (lo + 1 < P.tn && P.ttab[3 * (lo + 1)] <= e0) ++lo;
-    const int64_t base = P.ttab[3 * lo], numel = P.ttab[3 * lo + 1];
-    if (!P.tany || e0 < base || e0 >= base + numel) return 0u;
-    uint2 key = P.tkey;
-    uint64_t off0 = P.toff0;
-    if (P.tseedoff) {
-        const uint64_t sd = P.tseedoff[0];
-        key = make_uint2((uint32_t)sd, (uint32_t)(sd >> 32));
-        off0 = P.tseedoff[1];
-    }
-    const uint64_t ctr = (off0 + (uint64_t)lo * P.tstep) >> 2;
-    const int64_t rel = e0 - base;
-    const uint64_t t = (uint64_t)rel >> 2;
-    const uint4 w = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)), key);
-    uint32_t b = (uint32_t)(w.x <= P.tthr) | ((uint32_t)(w.y <= P.tthr) << 1) | ((uint32_t)(w.z <= P.tthr) << 2) |
-                 ((uint32_t)(w.w <= P.tthr) << 3);
-    const int64_t rem = numel - rel;
-    return rem >= 4 ? b : b & ((1u << rem) - 1u);
-}
-
-template <int SRC>
-__global__ __launch_bounds__(kSpBlock) void adam_sparta_rows_kernel(Pred P, int64_t n, float* __restrict__ param,
-                                                                   float* __restrict__ grad, float* __restrict__ m_,
-                                                                   float* __restrict__ v_, int K, int64_t ld,
-                                                                   AdamParams ap, const float* __restrict__ clip_coef,
-                                                                   float divisor) {
-    __shared__ uint64_t tab[kGapTable];
-    if (SRC != 1) load_gap_table(P, tab);
-    const int lane = threadIdx.x & 63;
-    const int64_t blk = (int64_t)blockIdx.x * kSpBlock;  // the workgroup's first vector
-    const int64_t i = blk + threadIdx.x;
-    const int64_t e0 = 4 * i;
-    const bool live = e0 < n;
-    uint32_t sel = 0;
-    if constexpr (SRC == 1) {
-        if (live) sel = torch_bits4(P, e0);
-    } else {
-        uint64_t w = 0;
-        if ((lane & 15) == 0 && live) w = pred_bits64<2>(P, tab, e0, n);
-        const int src = lane & ~15;
-        w = ((uint64_t)(uint32_t)__shfl((int)(w >> 32), src, 64) << 32) | (uint32_t)__shfl((int)w, src, 64);
-        sel = (uint32_t)(w >> (4 * (lane & 15))) & 0xFu;
-    }
-    if (!live) return;
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    const uint32_t o = (uint32_t)threadIdx.x;
-    // replica k+1's four vectors are loaded before replica k's stores (in flight together)
-    float4 p = stream_load(reinterpret_cast<const float4*>(param) + i);
-    float4 g = stream_load(reinterpret_cast<const float4*>(grad) + i);
-    float4 m = stream_load(reinterpret_cast<const float4*>(m_) + i);
-    float4 v = stream_load(reinterpret_cast<const float4*>(v_) + i);
-    for (int k = 0; k < K; ++k) {
-        const int64_t rk = (int64_t)k * ld;
-        float4 pn, gn, mn, vn;
-        if (k + 1 < K) {
-            const int64_t r1 = rk + ld;
-            pn = stream_load(reinterpret_cast<const float4*>(param + r1) + i);
-            gn = stream_load(reinterpret_cast<const float4*>(grad + r1) + i);
-            mn = stream_load(reinterpret_cast<const float4*>(m_ + r1) + i);
-            vn = stream_load(reinterpret_cast<const float4*>(v_ + r1) + i);
-        }
-        const float coef = clip_coef ? clip_coef[2 * k] : 1.f;
-        if (coef < 1.f) {
-            g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
-            stream_store(reinterpret_cast<float4*>(grad + rk) + i, g);  // clip_grad_norm_ leaves the clipped grads
-        }
-        float gg[4] = {g.x, g.y, g.z, g.w};
-        float pp[4] = {p.x, p.y, p.z, p.w}, mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            adam_elem(pp[e], gg[e], mm[e], vv[e], ap);
-            s[e] += pp[e];
-        }
-        *(reinterpret_cast<float4*>(param + rk) + i) = make_float4(pp[0], pp[1], pp[2], pp[3]);
-        store_sc1(reinterpret_cast<float4*>(m_ + rk) + blk, o, make_float4(mm[0], mm[1], mm[2], mm[3]));
-        store_sc1(reinterpret_cast<float4*>(v_ + rk) + blk, o, make_float4(vv[0], vv[1], vv[2], vv[3]));
-        if (k + 1 < K) {
-            p = pn;
-            g = gn;
-            m = mn;
-            v = vn;
-        }
-    }
-    if (sel) {  // ~2% of the lanes at p = 0.005
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if (!((sel >> e) & 1u)) continue;
-            const float avg = s[e] / divisor;
-            for (int k = 0; k < K; ++k) param[(int64_t)k * ld + e0 + e] = avg;
-        }
-    }
-}
-
 static_assert(kSpWaves * kWTile == kSpTile, "select wave kernel: a workgroup is one count/scan tile");
 template <typename T, int KQ, int SRC>
 __global__ __launch_bounds__(64 * kSpWaves) GA_SP_WPE_ATTR void sparta_select_wave_kernel(
@@ -1420,45 +1299,4 @@ extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32
         default: set_error("ga_sparta_scatter: unknown dtype %d", dtype); return GA_EINVAL;
     }
     return check_launch("ga_sparta_scatter");
-}
-
-extern "C" GA_API int ga_adam_sparta_step(int dtype, void* param, void* grad, float* exp_avg, float* exp_avg_sq,
-                                          int64_t K, int64_t ld, int64_t n, float lerp_w, float beta2,
-                                          float one_m_beta2, float eps, float wd_factor, float l2_wd,
-                                          float step_size, float bc2_sqrt, const float* clip_coef,
-                                          const void* mask, int mask_format, uint64_t seed, uint64_t iteration,
-                                          double p, const int64_t* skip, int64_t nskip, float divisor,
-                                          hipStream_t stream) {
-    clear_error();
-    GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX && n % 4 == 0, "ga_adam_sparta_step: n=%lld (a multiple of 4 "
-               "below 2^31)", (long long)n);
-    GA_REQUIRE(K >= 1 && K <= 65535, "ga_adam_sparta_step: bad K=%lld", (long long)K);
-    if (n == 0) return GA_OK;
-    GA_REQUIRE(K == 1 || (ld >= n && ld % 4 == 0), "ga_adam_sparta_step: ld must be >= n and a multiple of 4");
-    GA_REQUIRE(param && grad && exp_avg && exp_avg_sq, "ga_adam_sparta_step: null buffer");
-    GA_REQUIRE(dtype == GA_F32, "ga_adam_sparta_step: only float32 arenas are fused (dtype %d)", dtype);
-    GA_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
-               "ga_adam_sparta_step: buffers must be 16-byte aligned");
-    GA_REQUIRE(bc2_sqrt > 0.f, "ga_adam_sparta_step: bc2_sqrt must be > 0");
-    GA_REQUIRE(divisor > 0.0f, "ga_adam_sparta_step: divisor must be > 0");
-    GA_REQUIRE(p >= 0.0 && p <= 1.0, "ga_adam_sparta_step: p=%g outside [0, 1]", p);
-    GA_REQUIRE(mask_format == GA_MASK_BYTES || mask_format == GA_MASK_BITS || mask_format == GA_MASK_TORCH,
-               "ga_adam_sparta_step: bad mask_format %d", mask_format);
-    GA_REQUIRE(mask == nullptr || mask_format == GA_MASK_TORCH || ((uintptr_t)mask % 16) == 0,
-               "ga_adam_sparta_step: mask alignment");
-    GA_REQUIRE(mask_format != GA_MASK_TORCH || (mask && ((const ga_sparta_torch_draw*)mask)->table &&
-                                                ((const ga_sparta_torch_draw*)mask)->ntens > 0 &&
-                                                ((const ga_sparta_torch_draw*)mask)->offset0 % 4 == 0),
-               "ga_adam_sparta_step: bad ga_sparta_torch_draw");
-    GA_REQUIRE(nskip >= 0 && nskip < (1 << 24) && (nskip == 0 || skip), "ga_adam_sparta_step: bad skip table");
-    const Pred P = make_pred(mask, mask_format, seed, iteration, p, skip, nskip);
-    const AdamParams ap{lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size, bc2_sqrt};
-    const dim3 grid((unsigned)ceil_div(n / 4, (int64_t)kSpBlock));
-    if (P.ttab)
-        hipLaunchKernelGGL(adam_sparta_rows_kernel<1>, grid, dim3(kSpBlock), 0, stream, P, n, (float*)param,
-                           (float*)grad, exp_avg, exp_avg_sq, (int)K, ld, ap, clip_coef, divisor);
-    else
-        hipLaunchKernelGGL(adam_sparta_rows_kernel<2>, grid, dim3(kSpBlock), 0, stream, P, n, (float*)param,
-                           (float*)grad, exp_avg, exp_avg_sq, (int)K, ld, ap, clip_coef, divisor);
-    return check_launch("ga_adam_sparta_step");
 }

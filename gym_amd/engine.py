@@ -230,7 +230,7 @@ class DiLoCoOuter:
         at different physical addresses run the GPT-2 124M x 8 step at 1.65 ms
         or 1.88 ms, and the same virtual layout lands in either mode from one
         process to the next (tools/ubench_diloco_layout.cpp,
-        profiles/r04b_placement_search.txt, r04c_placement_sweep.txt) -- the
+        profiles/r04b_placement_search_p*.txt, r04c_placement_sweep.txt) -- the
         between-process spread of rounds 1-3.  So PLACEMENT_CANDIDATES
         separately allocated master+momentum buffers are timed once against the
         live replica set with ga_probe_diloco_placement (the step's exact access

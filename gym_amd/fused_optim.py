@@ -140,12 +140,7 @@ class ArenaAdam(torch.optim.Optimizer):
         return [(a, b) for a, b in out]
 
     @torch.no_grad()
-    def step(self, closure=None, max_norm=None, sparta=None):
-        """sparta: None, or the replica loop's single-process SPARTA average of
-        the new parameters, dict(divisor=..., and mask=... or seed/iteration/p/
-        skip as ops.sparta_average_local takes them): over full [K, ld] rows it
-        runs in the same pass as the optimizer (ops.adam_sparta_step), else as
-        the optimizer step followed by ops.sparta_average_local."""
+    def step(self, closure=None, max_norm=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -168,17 +163,10 @@ class ArenaAdam(torch.optim.Optimizer):
             ops.grad_clip_coef(self.G, self.ld, max_norm, self._partials, self._clip)
             clip = self._clip
         if all(r == [(0, self.ld)] for r in ranges):
-            if sparta is not None and self.ld % 4 == 0:
-                ops.adam_sparta_step(self.P, self.G, self.M, self.V, clip_coef=clip, **sparta, **hp)
-                return loss
             ops.adam_step(self.P, self.G, self.M, self.V, clip_coef=clip, **hp)
-        else:
-            for k in range(self.K):
-                ck = clip[2 * k:2 * k + 2] if clip is not None else None
-                for a, b in ranges[k]:
-                    ops.adam_step(self.P[k, a:b], self.G[k, a:b], self.M[k, a:b], self.V[k, a:b], clip_coef=ck,
-                                  **hp)
-        if sparta is not None:
-            kw = dict(sparta)
-            ops.sparta_average_local(self.P, self.ld, kw.pop("divisor"), layout="rows", **kw)
+            return loss
+        for k in range(self.K):
+            ck = clip[2 * k:2 * k + 2] if clip is not None else None
+            for a, b in ranges[k]:
+                ops.adam_step(self.P[k, a:b], self.G[k, a:b], self.M[k, a:b], self.V[k, a:b], clip_coef=ck, **hp)
         return loss

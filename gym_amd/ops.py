@@ -446,29 +446,4 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps,
                              float(step_size), float(bc2_sqrt), _p(clip_coef), _stream()), "ga_adam_step")
 
 
-def adam_sparta_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd,
-                     step_size, bc2_sqrt, divisor, clip_coef=None, mask=None, seed=0, iteration=0, p=0.0, skip=None,
-                     n=None):
-    """adam_step over fp32 [K, ld] rows fused with the single-process SPARTA
-    average of the new parameters (mask as sparta_average_local): bit-identical
-    to adam_step followed by sparta_average_local(layout="rows")."""
-    ts = [_as2d(t) for t in (param, grad, exp_avg, exp_avg_sq)]
-    _gpu(*ts, clip_coef, None if isinstance(mask, TorchDraw) else mask, skip)
-    K, ld = _rows_ld(ts[0])
-    for t in ts:
-        if t.dtype != torch.float32 or t.shape != ts[0].shape or t.stride() != ts[0].stride() or t.stride(-1) != 1:
-            raise ValueError("adam_sparta_step: param/grad/exp_avg/exp_avg_sq must be fp32 replica sets of one layout")
-    n = ts[0].shape[1] if n is None else int(n)
-    if clip_coef is not None and clip_coef.numel() < 2 * K:
-        raise ValueError("adam_sparta_step: clip_coef must hold 2 floats per replica")
-    skip, nskip = _skip_table(skip)
-    mask, mfmt = _mask_arg(mask, n, "adam_sparta_step")
-    thr = _rate(p, mask)
-    check(lib().ga_adam_sparta_step(_GA_F32, _p(ts[0]), _p(ts[1]), _p(ts[2]), _p(ts[3]), K, ld, n, float(lerp_w),
-                                    float(beta2), float(one_m_beta2), float(eps), float(wd_factor), float(l2_wd),
-                                    float(step_size), float(bc2_sqrt), _p(clip_coef), _mptr(mask), mfmt,
-                                    int(seed) & (2**64 - 1), int(iteration) & (2**64 - 1), thr, _p(skip), nskip,
-                                    float(divisor), _stream()), "ga_adam_sparta_step")
-
-
 _GA_F32 = _lib.GA_F32

@@ -15,10 +15,11 @@ batch_size // minibatch_size minibatches with `grad /= batch_size /
 minibatch_size`, its own clip_grad_norm_, then the strategy step.  Supported
 strategies: SimpleReduce, DiLoCo (SGD-family outer optimizer), SPARTA (every
 selector: the torch-drawn masks of node 0 -- the reference uses rank 0's --
-or the Philox stream), FedAvg without islands, DeMo.  Anything else runs on
+or the Philox stream), FedAvg (full or island averaging), DeMo.  Anything else runs on
 the process-per-node path (ReplicaRunner.supports).
 """
 import copy
+import random
 
 import numpy as np
 import torch
@@ -73,7 +74,7 @@ class ReplicaRunner:
         if isinstance(strategy, SPARTAStrategy):
             return True
         if isinstance(strategy, FedAvgStrategy):
-            return strategy.island_size is None
+            return True
         if isinstance(strategy, DiLoCoStrategy):
             return fused_sgd_hparams(strategy.outer_optim_spec) is not None
         return isinstance(strategy, (SimpleReduceStrategy, DeMoStrategy))
@@ -124,8 +125,13 @@ class ReplicaRunner:
                 self.outer.init_master(self.ra.flat_set[0])
             else:
                 self.max_norm = s.max_norm
-            if isinstance(s, (SimpleReduceStrategy, FedAvgStrategy)):
+            self.islands = (isinstance(s, FedAvgStrategy) and s.island_size is not None
+                            and s.island_size < num_nodes)
+            if isinstance(s, (SimpleReduceStrategy, FedAvgStrategy)) and not self.islands:
                 self.mean = MeanReduce(self.coll, self.K, ld, dev, dt)
+            if self.islands:
+                self._isl_row = torch.empty(1, ld, device=dev, dtype=dt)
+                self._isl_all = None  # [num_nodes, ld]: every node's parameters, gathered (processes > 1)
             elif isinstance(s, SPARTAStrategy):
                 self.sparta = Sparta(self.coll, self.K, ld, dev, dt, s.index_selector.p)
                 sel = s.index_selector
@@ -169,30 +175,22 @@ class ReplicaRunner:
             if s.local_step % s.H == 0 and s.local_step > 0:
                 self.outer(P)
         elif isinstance(s, SPARTAStrategy):
-            if self._fused_sparta():
-                # inner AdamW and the sparse average in one pass (ga_adam_sparta_step): the
-                # masks are drawn first -- the optimizer consumes no random numbers, so the
-                # generator ends where the reference's optim.step() + communicate leave it
-                if self.philox:
-                    kw = dict(seed=self.seed, iteration=self.iteration, p=s.index_selector.p,
-                              skip=self._skip_table())
-                else:
-                    kw = dict(mask=self._build_mask())
-                self.optim.step(max_norm=self.max_norm or None, sparta=dict(divisor=float(self.num_nodes), **kw))
+            self._inner()
+            if self.philox:
+                self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
             else:
-                self._inner()
-                if self.philox:
-                    self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
-                else:
-                    sel = s.index_selector
-                    m = self._build_mask()
-                    self.sparta(P, mask=m, mask_cap=self.sparta.cap if type(sel) is RandomIndexSelector else None,
-                                mask_shared=self.mask_shared)
+                sel = s.index_selector
+                m = self._build_mask()
+                self.sparta(P, mask=m, mask_cap=self.sparta.cap if type(sel) is RandomIndexSelector else None,
+                            mask_shared=self.mask_shared)
             self.iteration += 1
         elif isinstance(s, FedAvgStrategy):
             self._inner()
             if s.local_step % s.H == 0 and s.local_step > 0:
-                self.mean(P)
+                if self.islands:
+                    self._island_average(P)
+                else:
+                    self.mean(P)
         for sch in self.lr_scheds:
             sch.step()
         if self.rank == 0 and self.lr_scheds:
@@ -200,13 +198,36 @@ class ReplicaRunner:
                 cb(self.lr_scheds[0].get_last_lr()[0])
         s.local_step += 1
 
-    # the single-process SPARTA step fused into the inner AdamW launch (tests turn it off to
-    # compare against the two-launch path)
-    fuse_sparta = True
-
-    def _fused_sparta(self):
-        return (self.fuse_sparta and isinstance(self.optim, ArenaAdam) and not self.coll.exchange
-                and self.ra.dtype == torch.float32 and self.ra.ld % 4 == 0)
+    def _island_average(self, P):
+        """FedAvg islands (federated_averaging.py:26-69) over the nodes of this
+        process: the first process shuffles the node ids with Python's `random`
+        (the reference's rank 0 draw) and broadcasts them; every island is the
+        ascending-node fp32 sum of its members over its size (ga_replica_mean
+        through a row table, one launch per island), written to the members this
+        process hosts.  With several processes each first all-gathers every
+        node's parameters (the reference's all_gather), so islands may span them."""
+        N, s = self.num_nodes, self.s.island_size
+        ranks = list(range(N)) if self.rank == 0 else [None] * N
+        if self.rank == 0:
+            random.shuffle(ranks)
+        if self.coll.world > 1:
+            dist.broadcast_object_list(ranks, src=0)
+        src = P
+        if self.coll.exchange:
+            if self._isl_all is None:
+                self._isl_all = torch.empty(N, self.ra.ld, device=P.device, dtype=P.dtype)
+            self.coll.all_gather_into(self._isl_all.view(-1), P.reshape(-1))
+            src = self._isl_all
+        lo, hi = self.first_node, self.first_node + self.K
+        for i in range(0, N, s):
+            members = sorted(ranks[i:i + s])
+            mine = [m for m in members if lo <= m < hi]
+            if not mine:
+                continue
+            rows = torch.tensor(members, dtype=torch.int32, device=P.device)
+            ops.replica_mean(src, self._isl_row, rows=rows, divisor=float(len(members)))
+            for m in mine:
+                ops.replica_mean(self._isl_row, P[m - lo:m - lo + 1], divisor=1.0)
 
     def _grad_less(self):
         """Indices of node 0's tensors without a gradient (skipped, sparta.py:29-30)."""

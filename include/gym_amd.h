@@ -128,7 +128,7 @@ GA_API int ga_probe_chunk_stream(float* a, float* b, int64_t rows, int64_t cols,
  * kernel's own loads and stores -- with every value unchanged.  On MI355X the
  * step's rate depends on where master / momentum sit physically relative to the
  * replicas (1.65 vs 1.88 ms at GPT-2 124M x 8 for the same virtual layout,
- * profiles/r04b_placement_search.txt); DiLoCoOuter times candidate buffers with
+ * profiles/r04b_placement_search_p*.txt); DiLoCoOuter times candidate buffers with
  * this probe once and keeps the fastest (gym_amd/engine.py).
  */
 GA_API int ga_probe_diloco_placement(float* src, int64_t K, int64_t ld_src, int64_t n, float* master, float* mom,
@@ -423,28 +423,6 @@ GA_API int ga_adam_step(int dtype, void* param, void* grad, float* exp_avg, floa
                         int64_t ld, int64_t n, float lerp_w, float beta2, float one_m_beta2, float eps,
                         float wd_factor, float l2_wd, float step_size, float bc2_sqrt, const float* clip_coef,
                         hipStream_t stream);
-
-/*
- * The replica loop's SPARTA step (every node a local replica of one process,
- * no exchange) fused with its inner optimizer: ga_adam_step over the K
- * replicas, and then, for every element selected by the mask (as
- * ga_sparta_average_local: mask / mask_format / seed / iteration / p / skip),
- * every replica's parameter <- (ascending-replica fp32 sum of the K new
- * parameters) / divisor.  Bit-identical to ga_adam_step followed by
- * ga_sparta_average_local on the [K, ld] rows, in one streaming pass (the
- * sums come from the optimizer's own pass; no random word reads).  fp32,
- * n a multiple of 4.
- * Replaces: CommunicateOptimizeStrategy.step's `self.optim.step()` followed by
- * SparseCommunicator.communicate (communicate_optimize_strategy.py:67-85,
- * sparta.py:24-44) for batched replicas.
- */
-GA_API int ga_adam_sparta_step(int dtype, void* param, void* grad, float* exp_avg, float* exp_avg_sq,
-                               int64_t K, int64_t ld, int64_t n, float lerp_w, float beta2,
-                               float one_m_beta2, float eps, float wd_factor, float l2_wd,
-                               float step_size, float bc2_sqrt, const float* clip_coef,
-                               const void* mask, int mask_format, uint64_t seed, uint64_t iteration,
-                               double p, const int64_t* skip, int64_t nskip, float divisor,
-                               hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,7 @@ in-kernel ascending sums vs gloo's ring order).  CPU runs use the oracle
 stand-ins of tests/fake_ops.py; GPU runs the real kernels.
 """
 import os
+import random
 
 import numpy as np
 import torch
@@ -45,6 +46,8 @@ def make_strategy(name):
         return SPARTAStrategy(inner_optim=OptimSpec(torch.optim.AdamW, lr=1e-2), p_sparta=0.1, mask_source="philox")
     if name == "fedavg":
         return FedAvgStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.05), H=2, max_norm=0.5)
+    if name == "fedavg_islands":  # 3 nodes in islands of 2: a pair and a node alone, reshuffled every round
+        return FedAvgStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.05), island_size=2, H=1, max_norm=0.5)
     if name == "demo":
         return DeMoStrategy(lr=1e-2, compression_topk=8)
     raise KeyError(name)
@@ -72,6 +75,7 @@ def _proc_worker(rank, world, port, name, device, fake, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.manual_seed(42)
+        random.seed(1234)  # FedAvg islands: rank 0's partner draw
         dev = torch.device(device)
         model = _model(name, dev)
         s = make_strategy(name)
@@ -100,6 +104,7 @@ def run_replica_mode(name, K, device, fake):
     """All K nodes in this process (no process group: world 1)."""
     from gym_amd.replica import ReplicaRunner
     torch.manual_seed(42)
+    random.seed(1234)  # FedAvg islands: the first process's partner draw, as rank 0's
     dev = torch.device(device)
     models = [_model(name, dev) for _ in range(K)]
     runner = ReplicaRunner(make_strategy(name), models, rank=0, num_nodes=K)
@@ -109,6 +114,45 @@ def run_replica_mode(name, K, device, fake):
             _set_grads(m, k, t, dev)
         runner.step()
     return [[p.detach().float().cpu().numpy() for p in m.parameters()] for m in models]
+
+
+def _replica_worker(rank, world, K, port, name, device, fake, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    if fake:
+        import fake_ops
+        fake_ops.install()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gym_amd.replica import ReplicaRunner
+        torch.manual_seed(42)
+        random.seed(1234)
+        dev = torch.device(device)
+        models = [_model(name, dev) for _ in range(K)]
+        runner = ReplicaRunner(make_strategy(name), models, rank=rank, num_nodes=world * K)
+        for t in range(STEPS):
+            runner.zero_grad()
+            for k, m in enumerate(models):
+                _set_grads(m, rank * K + k, t, dev)
+            runner.step()
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"),
+                 **{f"p_{k}_{i}": p.detach().float().cpu().numpy() for k, m in enumerate(models)
+                    for i, p in enumerate(m.parameters())})
+    finally:
+        dist.destroy_process_group()
+
+
+def run_replica_processes(name, world, K, device, fake, out_dir):
+    """world processes over gloo, each hosting K nodes (node = rank * K + k)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_replica_worker, args=(world, K, free_port(), name, device, fake, out_dir), nprocs=world, join=True)
+    res = []
+    for r in range(world):
+        with np.load(os.path.join(out_dir, f"r{r}.npz")) as f:
+            for k in range(K):
+                res.append([f[f"p_{k}_{i}"] for i in range(len(SHAPES))])
+    return res
 
 
 def compare(proc, rep, rtol=1e-5, atol=2e-6):

@@ -9,7 +9,8 @@ import replica_scenarios as R
 
 pytestmark = pytest.mark.gpu
 
-NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "demo", "demo_frozen", "sparta_frozen"]
+NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "fedavg_islands", "demo", "demo_frozen",
+         "sparta_frozen"]
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -18,9 +19,10 @@ def test_replicas_match_process_per_node_gpu(tmp_path, name):
         pytest.skip("no GPU")
     proc = R.run_process_mode(name, 3, "cuda:0", False, str(tmp_path))
     rep = R.run_replica_mode(name, 3, "cuda:0", False)
-    if name.startswith("demo"):
-        # the same kernels on the same payloads (node order), one launch for K
-        # replicas or K launches of one: identical bits
+    if name.startswith("demo") or name == "fedavg_islands":
+        # DeMo: the same kernels on the same payloads (node order), one launch for K
+        # replicas or K launches of one; FedAvg islands: the ascending-member fp32
+        # sum / size on both paths: identical bits
         R.compare(proc, rep, rtol=0, atol=0)
         return
     R.compare(proc, rep)

@@ -7,7 +7,8 @@ import pytest
 
 import replica_scenarios as R
 
-NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "demo", "demo_frozen", "sparta_frozen"]
+NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "fedavg_islands", "demo", "demo_frozen",
+         "sparta_frozen"]
 
 
 @pytest.fixture
@@ -31,6 +32,17 @@ def fake(monkeypatch):
 def test_replicas_match_process_per_node(tmp_path, fake, name):
     proc = R.run_process_mode(name, 3, "cpu", True, str(tmp_path))
     rep = R.run_replica_mode(name, 3, "cpu", True)
+    R.compare(proc, rep)
+
+
+@pytest.mark.parametrize("name", ["fedavg_islands", "simple"])
+def test_replica_processes_match_process_per_node(tmp_path, name):
+    """2 processes x 2 local nodes (gloo) == 4 processes of one node: FedAvg
+    islands spanning the processes (the all-gather path) and the full average."""
+    (tmp_path / "p").mkdir()
+    (tmp_path / "r").mkdir()
+    proc = R.run_process_mode(name, 4, "cpu", True, str(tmp_path / "p"))
+    rep = R.run_replica_processes(name, 2, 2, "cpu", True, str(tmp_path / "r"))
     R.compare(proc, rep)
 
 
