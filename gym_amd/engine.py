@@ -165,8 +165,10 @@ class MeanReduce:
             ops.replica_mean(self.sum, reps, n=n, divisor=self.K_total)
 
 
-# master+momentum buffers timed against the replica set before the first outer step
-PLACEMENT_CANDIDATES = 6
+# physical master+momentum candidates (gym_amd.placement) timed against the replica set
+# before the first outer step; the fastest is kept
+PLACEMENT_CANDIDATES = 64
+PLACEMENT_MAX_FRAC = 0.3  # of the free device memory the candidates may take at once
 
 
 class DiLoCoOuter:
@@ -197,6 +199,7 @@ class DiLoCoOuter:
         self.mom = self._state[self.per:] if momentum != 0 else None
         self.placement = None  # the placement probe's record (bench / DESIGN)
         self._placed_for = None
+        self._placed = None  # the PlacedBuffer holding the state, when one was chosen
         self.first = True
         self.dtype = dtype
         self.sum = torch.empty(n, device=device, dtype=dtype) if (X and not self.shard) else None
@@ -223,20 +226,20 @@ class DiLoCoOuter:
         self._outer(rs_shard, self.K_total, own, m[0], m[1])
 
     def _place(self, reps):
-        """Choose where master / momentum live, once per replica set.
+        """Choose the physical memory master / momentum live in, once per replica set.
 
-        On MI355X the fused step's rate depends on the PHYSICAL placement of
-        its 2K + 4 streams: with the replica set fixed, master/momentum buffers
-        at different physical addresses run the GPT-2 124M x 8 step at 1.65 ms
-        or 1.88 ms, and the same virtual layout lands in either mode from one
-        process to the next (tools/ubench_diloco_layout.cpp,
-        profiles/r04b_placement_search_p*.txt, r04c_placement_sweep.txt) -- the
-        between-process spread of rounds 1-3.  So PLACEMENT_CANDIDATES
-        separately allocated master+momentum buffers are timed once against the
-        live replica set with ga_probe_diloco_placement (the step's exact access
-        pattern, every value written back unchanged: ~2 ms per launch, three
-        launches per candidate) and the fastest is kept; the state is copied
-        into it and the others are freed."""
+        On MI355X the fused step's rate depends on where its 2K + 4 streams sit
+        PHYSICALLY (gym_amd.placement: regions of several GB map to the HBM
+        channels/banks differently; master/momentum in a region that maps like
+        the replica set's make the step 1.88 instead of 1.57-1.65 ms at GPT-2
+        124M x 8, and which one an allocation gets changes from process to
+        process: the between-process spread of rounds 1-3).  So up to
+        PLACEMENT_CANDIDATES physical allocations (hipMemCreate, one at a time,
+        each mapped on its own) are timed once against the live replica set with
+        ga_probe_diloco_placement -- the step's exact access pattern, every value
+        written back unchanged -- beside the ordinary allocation; the fastest
+        keeps the state, the others are released.  ~0.2 s once; at most
+        PLACEMENT_MAX_FRAC of the free memory at a time."""
         key = (reps.data_ptr(), reps.stride(0))
         if self._placed_for == key:
             return
@@ -246,28 +249,46 @@ class DiLoCoOuter:
                 or reps.shape[0] > 16 or 4 * per < SHARD_MIN_BYTES or PLACEMENT_CANDIDATES < 2
                 or reps.stride(1) != 1 or reps.stride(0) % 4 or per % 4):
             return
-        cands = [self._state] + [torch.empty(2 * per, device=reps.device, dtype=torch.float32)
-                                 for _ in range(PLACEMENT_CANDIDATES - 1)]
+        from .placement import PlacedBuffer
         src = reps[:, :per]
-        times = []
-        for c in cands:
-            ops.probe_diloco_placement(src, per, c[:per], c[per:])  # warm-up
+
+        def probe(state):
+            ops.probe_diloco_placement(src, per, state[:per], state[per:2 * per])  # warm-up
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(3):
-                ops.probe_diloco_placement(src, per, c[:per], c[per:])
+                ops.probe_diloco_placement(src, per, state[:per], state[per:2 * per])
             e1.record()
             e1.synchronize()
-            times.append(e0.elapsed_time(e1) / 3)
-        best = min(range(len(cands)), key=lambda i: times[i])
-        if best != 0:
-            cands[best].copy_(self._state)
-            self._state = cands[best]
-            self.master, self.mom = self._state[:per], self._state[per:]
-        del cands, src
-        torch.cuda.empty_cache()  # the losing candidates go back to the driver
-        self.placement = {"candidates": PLACEMENT_CANDIDATES, "probe_ms": [round(t, 4) for t in times],
-                          "chosen": best}
+            return e0.elapsed_time(e1) / 3
+
+        times = [probe(self._state)]
+        best, best_t, best_buf = 0, times[0], None
+        budget = PLACEMENT_MAX_FRAC * torch.cuda.mem_get_info(reps.device)[0]
+        held = []  # every candidate stays allocated until the choice is made (distinct physical memory)
+        try:
+            while len(times) < PLACEMENT_CANDIDATES and (len(held) + 1) * 8 * per <= budget:
+                buf = PlacedBuffer(8 * per, reps.device)
+                held.append(buf)
+                t = probe(buf.tensor())
+                times.append(t)
+                if t < best_t:
+                    best, best_t, best_buf = len(times) - 1, t, buf
+        except RuntimeError:  # no VMM on this device / out of memory: keep what was probed
+            pass
+        if best_buf is not None:
+            st = best_buf.tensor()[:2 * per]
+            st.copy_(self._state)
+            self._state, self._placed = st, best_buf
+            self.master, self.mom = st[:per], st[per:]
+        for b in held:
+            if b is not best_buf:
+                b.release()
+        del held, src
+        torch.cuda.empty_cache()
+        self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
+                          "how": "master+momentum in physical allocations (hipMemCreate) probed with the step's "
+                                 "access pattern; candidate 0 = the ordinary allocation"}
 
     def __call__(self, reps):
         n = self.n

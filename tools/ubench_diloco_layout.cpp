@@ -166,12 +166,52 @@ static int sweep(int reps, hipStream_t s) {
     return 0;
 }
 
+// map mode: a 100 GiB pool; (A) the replica set in its own allocation (as the product
+// allocates it), master + momentum adjacent at 2 GiB steps over the pool; (B) the
+// replica set at pool offset R (8 GiB steps), master + momentum at pool offset M
+// (8 GiB steps): the (R, M) grid of step times
+static int map_mode(int reps, hipStream_t s) {
+    const int64_t G1 = 1LL << 30;
+    const int64_t pool_bytes = 100 * G1;
+    const int64_t one_b = 4 * N, rows_b = 4 * K * N;
+    float* rep;
+    CK(hipMalloc(&rep, rows_b));
+    CK(hipMemset(rep, 0, rows_b));
+    char* pool;
+    CK(hipMalloc(&pool, pool_bytes));
+    CK(hipMemset(pool, 0, pool_bytes));
+    auto at = [&](int64_t off) { return (float*)(pool + off); };
+    auto t1 = [&](const Layout& L) { const float a = run(L, reps, s), b = run(L, reps, s); return a < b ? a : b; };
+    printf("A (replicas in their own allocation; master+mom at pool offset g GiB):\n");
+    for (int64_t g = 0; g + 1 < 100; g += 2) {
+        const float t = t1(Layout{"a", rep, N, at(g * G1), at(g * G1 + one_b)});
+        printf("  g=%3lld %.3f%s", (long long)g, t, (g / 2) % 8 == 7 ? "\n" : "");
+    }
+    printf("\nB (replicas at pool offset R GiB, master+mom at pool offset M GiB), ms:\n      ");
+    for (int64_t M = 0; M < 100; M += 8) printf(" M=%-4lld", (long long)M);
+    printf("\n");
+    for (int64_t R = 0; R + 4 < 100; R += 8) {
+        printf("R=%3lld", (long long)R);
+        for (int64_t M = 0; M < 100; M += 8) {
+            if (M + 1 > R && M < R + 5) {
+                printf("   --  ");
+                continue;
+            }
+            printf(" %.3f", t1(Layout{"b", at(R * G1), N, at(M * G1), at(M * G1 + one_b)}));
+        }
+        printf("\n");
+        fflush(stdout);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 4;
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     if (argc > 3 && !strcmp(argv[3], "sweep")) return sweep(reps, s);
+    if (argc > 3 && !strcmp(argv[3], "map")) return map_mode(reps, s);
     if (argc > 3 && !strcmp(argv[3], "search")) return search(argc > 4 ? atoi(argv[4]) : 0, argc > 5 ? atoi(argv[5]) : 40, reps, s);
     std::vector<Layout> Ls;
     // (a) the product's allocation: replica set, master, momentum as separate allocations
