@@ -321,3 +321,42 @@ def test_sparta_reference_draw_gpt2_124m_32_nodes():
     exp = torch.from_numpy(np.stack([osparta.sparse_average(list(em[j].cpu().numpy().reshape(K, 1)),
                                                             np.ones(1, bool))[0] for j in i.tolist()]).reshape(-1))
     assert torch.equal(outs[0][i, 0].cpu(), exp)
+
+
+def test_placed_buffer_round_trip_and_diloco_placement():
+    """gym_amd.placement: a physical allocation (hipMemCreate) mapped as a torch
+    tensor reads back what was written and is released; DiLoCoOuter's placement
+    probe leaves the replicas untouched and the outer step bit-identical to an
+    engine that kept its ordinary allocation."""
+    from gym_amd import engine as E
+    from gym_amd.comm import Collective
+    from gym_amd.placement import PlacedBuffer
+    b = PlacedBuffer(3 << 20, DEV)
+    t = b.tensor()
+    assert t.numel() * 4 >= 3 << 20 and t.is_cuda
+    t.copy_(torch.arange(t.numel(), device=DEV, dtype=torch.float32))
+    assert torch.equal(t[-5:].cpu(), torch.arange(t.numel() - 5, t.numel(), dtype=torch.float32))
+    b.release()
+    K = 4
+    n = (48 << 20) // 4  # 48 MB per replica: above the placement threshold
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    x0 = torch.randn(K, n, device=DEV, generator=g)
+    drift = torch.randn(K, n, device=DEV, generator=g) * 1e-3
+    outs = []
+    for cands in (64, 1):
+        old = E.PLACEMENT_CANDIDATES
+        E.PLACEMENT_CANDIDATES = cands
+        try:
+            x = x0.clone()
+            eng = E.DiLoCoOuter(Collective(), K, n, DEV, torch.float32)
+            eng.init_master(x[0])
+            for step in range(2):
+                eng(x)
+                x.add_(drift)
+            outs.append((x.clone(), eng.master.clone(), eng.mom.clone(), eng.placement))
+        finally:
+            E.PLACEMENT_CANDIDATES = old
+    assert outs[0][3] is not None and outs[0][3]["candidates"] >= 2
+    for a, b2 in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(a, b2)
