@@ -771,7 +771,10 @@ def bench_inner_adamw(args, coll, dev, model="gpt2-124m", max_norm=1.0):
     return {"model": model, "n": n, "ms_per_step": round(t * 1e3, 4), "kernel_ms": round(kern, 4),
             "kernel_GBps": round(alg / (kern * 1e-3) / 1e9, 1),
             "kernel_frac_hbm": round(alg / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "torch_adamw_foreach_ms": round(tt * 1e3, 4), "speedup_vs_torch": round(tt / t, 2)}
+            "torch_adamw_foreach_ms": round(tt * 1e3, 4), "speedup_vs_torch": round(tt / t, 2),
+            "placement": {k: v for k, v in (opt.placement or {}).items() if k != "probe_ms"} or None,
+            "placement_probe_ms_best_vs_ordinary": ([round(min(opt.placement["probe_ms"]), 4),
+                                                     opt.placement["probe_ms"][0]] if opt.placement else None)}
 
 
 def main():

@@ -70,6 +70,35 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ par
     }
 }
 
+// Placement probe of adam_kernel (no reference counterpart): its exact access pattern
+// (replicas on grid.y, 1024 float4 per workgroup, p, g, m, v read, p, m, v written
+// through the same stores) with every value written back unchanged, so ArenaAdam can
+// time candidate physical buffers for the moments without side effects.
+__global__ __launch_bounds__(kOptBlock) void adam_probe_kernel(float* __restrict__ param,
+                                                               const float* __restrict__ grad,
+                                                               float* __restrict__ m_, float* __restrict__ v_,
+                                                               int64_t n, int64_t ld) {
+    const int64_t rep = blockIdx.y;
+    param += rep * ld;
+    grad += rep * ld;
+    m_ += rep * ld;
+    v_ += rep * ld;
+    const int64_t nv = n >> 2;
+    const int64_t lo = (int64_t)blockIdx.x * kOptChunk;
+    const int64_t hi = lo + kOptChunk < nv ? lo + kOptChunk : nv;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kOptBlock) {
+        const float4 p = stream_load(reinterpret_cast<const float4*>(param) + i);
+        const float4 g = stream_load(reinterpret_cast<const float4*>(grad) + i);
+        const float4 m = stream_load(reinterpret_cast<const float4*>(m_) + i);
+        const float4 v = stream_load(reinterpret_cast<const float4*>(v_) + i);
+        const uint32_t o = (uint32_t)(i - lo);
+        asm volatile("" ::"v"(g.x), "v"(g.y), "v"(g.z), "v"(g.w));  // the grad load stays live
+        store_sc1(reinterpret_cast<float4*>(param) + lo, o, p);
+        store_sc1(reinterpret_cast<float4*>(m_) + lo, o, m);
+        store_sc1(reinterpret_cast<float4*>(v_) + lo, o, v);
+    }
+}
+
 // partials[b] = sum of x^2 over a grid-stride share of the arena (fp32, fixed order)
 template <typename T>
 __global__ __launch_bounds__(kOptBlock) void sumsq_kernel(const T* __restrict__ x, int64_t n, int64_t ld,
@@ -171,4 +200,21 @@ extern "C" GA_API int ga_adam_step(int dtype, void* param, void* grad, float* ex
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)grid, (unsigned)K), dim3(kOptBlock), 0, stream, (float*)param,
                        (float*)grad, exp_avg, exp_avg_sq, n, ld, ap, clip_coef);
     return check_launch("ga_adam_step");
+}
+
+extern "C" GA_API int ga_probe_adam_placement(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                                              int64_t K, int64_t ld, int64_t n, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(n >= 0 && n % 4 == 0 && K >= 1 && K <= 65535, "ga_probe_adam_placement: bad sizes n=%lld K=%lld",
+               (long long)n, (long long)K);
+    if (n == 0) return GA_OK;
+    GA_REQUIRE(K == 1 || (ld >= n && ld % 4 == 0), "ga_probe_adam_placement: ld must be >= n and a multiple of 4");
+    GA_REQUIRE(param && grad && exp_avg && exp_avg_sq, "ga_probe_adam_placement: null buffer");
+    GA_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+               "ga_probe_adam_placement: buffers must be 16-byte aligned");
+    int64_t grid = (n / 4 + kOptChunk - 1) / kOptChunk;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(adam_probe_kernel, dim3((unsigned)grid, (unsigned)K), dim3(kOptBlock), 0, stream, param, grad,
+                       exp_avg, exp_avg_sq, n, ld);
+    return check_launch("ga_probe_adam_placement");
 }

@@ -249,42 +249,22 @@ class DiLoCoOuter:
                 or reps.shape[0] > 16 or 4 * per < SHARD_MIN_BYTES or PLACEMENT_CANDIDATES < 2
                 or reps.stride(1) != 1 or reps.stride(0) % 4 or per % 4):
             return
-        from .placement import PlacedBuffer
+        from . import placement
         src = reps[:, :per]
 
-        def probe(state):
-            ops.probe_diloco_placement(src, per, state[:per], state[per:2 * per])  # warm-up
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(3):
-                ops.probe_diloco_placement(src, per, state[:per], state[per:2 * per])
-            e1.record()
-            e1.synchronize()
-            return e0.elapsed_time(e1) / 3
+        def probe_state(state):
+            return placement.time_probe(lambda: ops.probe_diloco_placement(src, per, state[:per], state[per:2 * per]))
 
-        times = [probe(self._state)]
-        best, best_t, best_buf = 0, times[0], None
-        budget = PLACEMENT_MAX_FRAC * torch.cuda.mem_get_info(reps.device)[0]
-        held = []  # every candidate stays allocated until the choice is made (distinct physical memory)
-        try:
-            while len(times) < PLACEMENT_CANDIDATES and (len(held) + 1) * 8 * per <= budget:
-                buf = PlacedBuffer(8 * per, reps.device)
-                held.append(buf)
-                t = probe(buf.tensor())
-                times.append(t)
-                if t < best_t:
-                    best, best_t, best_buf = len(times) - 1, t, buf
-        except RuntimeError:  # no VMM on this device / out of memory: keep what was probed
-            pass
+        best_buf, times = placement.choose(8 * per, reps.device, lambda b: probe_state(b.tensor()),
+                                           probe_state(self._state), PLACEMENT_CANDIDATES, PLACEMENT_MAX_FRAC)
+        best = 0
         if best_buf is not None:
+            best = min(range(len(times)), key=lambda i: times[i])
             st = best_buf.tensor()[:2 * per]
             st.copy_(self._state)
             self._state, self._placed = st, best_buf
             self.master, self.mom = st[:per], st[per:]
-        for b in held:
-            if b is not best_buf:
-                b.release()
-        del held, src
+        del src
         torch.cuda.empty_cache()
         self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
                           "how": "master+momentum in physical allocations (hipMemCreate) probed with the step's "

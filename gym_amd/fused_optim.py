@@ -25,6 +25,11 @@ from . import ops
 
 _UNSUPPORTED = ("amsgrad", "maximize", "capturable", "differentiable")
 
+# physical placement of the moments (gym_amd.placement), chosen on the first step
+PLACEMENT_CANDIDATES = 48
+PLACEMENT_MAX_FRAC = 0.3
+PLACEMENT_MIN_BYTES = 32 << 20
+
 
 def fusable(spec_cls, kwargs, arena):
     """True when OptimSpec(spec_cls, **kwargs) can run as ArenaAdam on this arena."""
@@ -94,6 +99,8 @@ class ArenaAdam(torch.optim.Optimizer):
             sp.sort(key=lambda t: t[1])
         self._partials = ops.sumsq_partials(dev, self.K)
         self._clip = torch.ones(2 * self.K, dtype=torch.float32, device=dev)
+        self._placed = None  # PlacedBuffer holding M and V once _place chose one
+        self.placement = None
 
     def _bind_state(self, p):
         k, o, n = self._where[id(p)]
@@ -125,6 +132,44 @@ class ArenaAdam(torch.optim.Optimizer):
         for p in self.param_groups[0]["params"]:
             self._bind_state(p)
 
+    def _place(self):
+        """Choose the physical memory of the moments, once, before the first
+        step: the fused step's rate depends on where exp_avg / exp_avg_sq sit
+        physically relative to the parameters and gradients (0.553-0.625 ms at
+        GPT-2 124M, profiles/r04k_adam_placement.txt; gym_amd.placement), so up
+        to PLACEMENT_CANDIDATES physical allocations are timed with
+        ga_probe_adam_placement (the step's access pattern, values unchanged)
+        beside the ordinary ones and the fastest keeps the moments."""
+        self._place_done = True
+        nb = 2 * self.M.numel() * 4
+        if (self.P.device.type != "cuda" or nb < PLACEMENT_MIN_BYTES or PLACEMENT_CANDIDATES < 2
+                or self.ld % 4 or self.P.stride(-1) != 1):
+            return
+        from . import placement
+        KL = self.K * self.ld
+
+        def probe(M, V):
+            return placement.time_probe(lambda: ops.probe_adam_placement(self.P, self.G, M, V))
+
+        def split(buf):
+            t = buf.tensor()
+            return t[:KL].view(self.K, self.ld), t[KL:2 * KL].view(self.K, self.ld)
+
+        best, times = placement.choose(nb, self.P.device, lambda b: probe(*split(b)), probe(self.M, self.V),
+                                       PLACEMENT_CANDIDATES, PLACEMENT_MAX_FRAC)
+        chosen = 0
+        if best is not None:
+            chosen = min(range(len(times)), key=lambda i: times[i])
+            M, V = split(best)
+            M.copy_(self.M)
+            V.copy_(self.V)
+            self.M, self.V, self._placed = M, V, best
+            self.exp_avg, self.exp_avg_sq = self.M.view(-1), self.V.view(-1)
+            for p in self.param_groups[0]["params"]:
+                self._bind_state(p)
+            torch.cuda.empty_cache()
+        self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": chosen}
+
     def _ranges(self, k):
         """Contiguous ranges [a, b) of replica k's arena whose parameters have a
         gradient now (the whole row when all do: the padding stays 0)."""
@@ -148,6 +193,8 @@ class ArenaAdam(torch.optim.Optimizer):
         ranges = [self._ranges(k) for k in range(self.K)]
         for ar in self.arenas:
             ar.sync_grads()
+        if not getattr(self, "_place_done", False):
+            self._place()
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = float(g["lr"]), g["betas"], float(g["eps"]), float(g["weight_decay"])
         decoupled = g["decoupled_weight_decay"]

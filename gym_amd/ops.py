@@ -412,6 +412,19 @@ def probe_diloco_placement(reps, n, master, mom):
           "ga_probe_diloco_placement")
 
 
+def probe_adam_placement(param, grad, exp_avg, exp_avg_sq):
+    """ga_adam_step's access pattern over fp32 [K, ld] sets of one layout, every
+    value written back unchanged (placement probe)."""
+    ts = [_as2d(t) for t in (param, grad, exp_avg, exp_avg_sq)]
+    _gpu(*ts)
+    K, ld = _rows_ld(ts[0])
+    for t in ts:
+        if t.dtype != torch.float32 or t.shape != ts[0].shape or t.stride() != ts[0].stride() or t.stride(-1) != 1:
+            raise ValueError("probe_adam_placement: fp32 replica sets of one layout")
+    check(lib().ga_probe_adam_placement(_p(ts[0]), _p(ts[1]), _p(ts[2]), _p(ts[3]), K, ld, ts[0].shape[1],
+                                        _stream()), "ga_probe_adam_placement")
+
+
 def sumsq_partials(device, K=1):
     return torch.empty(int(K) * int(lib().ga_sumsq_partials_count()), dtype=torch.float32, device=device)
 

@@ -1,4 +1,5 @@
-"""Physically placed device buffers (HIP virtual memory management).
+"""Physically placed device buffers (HIP virtual memory management), for the
+state buffers the strategy step owns (DiLoCo master/momentum, AdamW moments).
 
 On MI355X the fused DiLoCo step runs 1.57-1.65 ms or 1.88 ms for the same
 virtual layout (GPT-2 124M x 8 replicas), depending on where its streams sit
@@ -137,3 +138,42 @@ class PlacedBuffer:
             self.release()
         except Exception:
             pass
+
+
+def time_probe(fn, reps=3):
+    """ms per call of fn (one warm-up, then reps calls between two events)."""
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac):
+    """Create up to max_candidates - 1 physical allocations of nbytes one at a
+    time (all held until the choice is made, so each is distinct memory), time
+    probe(PlacedBuffer) on each, and return (the fastest PlacedBuffer, or None
+    when none beats baseline_ms -- the caller's ordinary allocation --, every
+    time in creation order with the baseline first).  At most max_frac of the
+    free device memory is taken; a device without virtual memory management, or
+    running out, ends the search with what was probed."""
+    times = [baseline_ms]
+    best, best_t, held = None, baseline_ms, []
+    budget = max_frac * torch.cuda.mem_get_info(torch.device(device))[0]
+    try:
+        while len(times) < max_candidates and (len(held) + 1) * nbytes <= budget:
+            buf = PlacedBuffer(nbytes, device)
+            held.append(buf)
+            t = probe(buf)
+            times.append(t)
+            if t < best_t:
+                best, best_t = buf, t
+    except RuntimeError:
+        pass
+    for b in held:
+        if b is not best:
+            b.release()
+    return best, times

@@ -134,6 +134,17 @@ GA_API int ga_probe_chunk_stream(float* a, float* b, int64_t rows, int64_t cols,
 GA_API int ga_probe_diloco_placement(float* src, int64_t K, int64_t ld_src, int64_t n, float* master, float* mom,
                                      hipStream_t stream);
 
+/*
+ * Placement probe (no reference counterpart) for the fused Adam/AdamW step:
+ * ga_adam_step's access pattern over fp32 [K, ld] param / grad / exp_avg /
+ * exp_avg_sq sets (n a multiple of 4, 16-byte aligned) -- p, g, m, v read, p, m,
+ * v written back unchanged.  ArenaAdam times candidate physical buffers for the
+ * moments with it once (the step ran 0.553-0.625 ms at GPT-2 124M by where they
+ * sit, profiles/r04k_adam_placement.txt).
+ */
+GA_API int ga_probe_adam_placement(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t K,
+                                   int64_t ld, int64_t n, hipStream_t stream);
+
 /* ---- mean reduce: SimpleReduce / FedAvg / DiLoCo averaging ------------- */
 
 /*
