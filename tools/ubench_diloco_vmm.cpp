@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../include/gym_amd.h"
@@ -58,6 +59,59 @@ static float run(float* rep, int64_t ld, float* master, float* mom, int reps, hi
     return best;
 }
 
+// (3) the replica set itself as K row chunks mapped into one VA range, with `spacer` GiB of
+// held physical memory created between consecutive rows (released after), then master+mom
+// probed over 24 candidates: best and median step time per spacer size
+static void rows_spread(hipStream_t s, const hipMemAllocationProp& prop, const hipMemAccessDesc& acc) {
+    const int64_t G1 = 1LL << 30;
+    const int64_t ld = (N + 1023) / 1024 * 1024;  // rows a multiple of 4 KiB
+    const int64_t row_b = 4 * ld;
+    for (int spacer : {0, 2, 4, 8}) {
+        void* va = nullptr;
+        CK(hipMemAddressReserve(&va, (size_t)(K * row_b), 2 << 20, nullptr, 0));
+        std::vector<hipMemGenericAllocationHandle_t> rows(K), sp;
+        for (int k = 0; k < K; ++k) {
+            CK(hipMemCreate(&rows[k], row_b, (hipMemAllocationProp*)&prop, 0));
+            CK(hipMemMap((char*)va + k * row_b, row_b, 0, rows[k], 0));
+            for (int j = 0; j < spacer && k + 1 < K; ++j) {
+                hipMemGenericAllocationHandle_t h;
+                CK(hipMemCreate(&h, G1, (hipMemAllocationProp*)&prop, 0));
+                sp.push_back(h);
+            }
+        }
+        CK(hipMemSetAccess(va, (size_t)(K * row_b), &acc, 1));
+        CK(hipMemset(va, 0, (size_t)(K * row_b)));
+        for (auto h : sp) CK(hipMemRelease(h));
+        std::vector<float> ts;
+        std::vector<std::pair<void*, hipMemGenericAllocationHandle_t>> cands;
+        for (int c = 0; c < 24; ++c) {
+            hipMemGenericAllocationHandle_t h;
+            void* cv = nullptr;
+            CK(hipMemCreate(&h, G1, (hipMemAllocationProp*)&prop, 0));
+            CK(hipMemAddressReserve(&cv, G1, 2 << 20, nullptr, 0));
+            CK(hipMemMap(cv, G1, 0, h, 0));
+            CK(hipMemSetAccess(cv, G1, &acc, 1));
+            cands.push_back({cv, h});
+            ts.push_back(run((float*)va, ld, (float*)cv, (float*)cv + N, 5, s));
+        }
+        std::vector<float> st = ts;
+        std::sort(st.begin(), st.end());
+        printf("(3) rows as chunks, %d GiB spacers: master+mom best %.3f median %.3f worst %.3f ms | ", spacer, st[0],
+               st[st.size() / 2], st.back());
+        for (float x : ts) printf("%.2f ", x);
+        printf("\n");
+        fflush(stdout);
+        for (auto& c : cands) {
+            CK(hipMemUnmap(c.first, G1));
+            CK(hipMemAddressFree(c.first, G1));
+            CK(hipMemRelease(c.second));
+        }
+        CK(hipMemUnmap(va, (size_t)(K * row_b)));
+        CK(hipMemAddressFree(va, (size_t)(K * row_b)));
+        for (auto h : rows) CK(hipMemRelease(h));
+    }
+}
+
 int main() {
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -71,6 +125,13 @@ int main() {
     size_t gran = 0;
     CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
     printf("VMM supported %d, granularity %zu B\n", vmm, gran);
+    if (getenv("ROWS_SPREAD")) {
+        hipMemAccessDesc acc0 = {};
+        acc0.location = prop.location;
+        acc0.flags = hipMemAccessFlagsProtReadWrite;
+        rows_spread(s, prop, acc0);
+        return 0;
+    }
     const int64_t G1 = 1LL << 30;
     const int nch = 48;
     void* va = nullptr;
