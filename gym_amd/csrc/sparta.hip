@@ -34,13 +34,25 @@ constexpr int kSelCap = 4096;                  // selected positions listed per 
 constexpr int kScanBlock = 1024;
 constexpr int kGapTable = 64;
 
+// a * b as one v_mad_u64_u32 (low and high words from one instruction); the
+// compiler's v_mul_lo_u32 + v_mul_hi_u32 pair runs Philox 20% slower
+// (tools/ubench_philox_mul.hip, profiles/r04n_philox_mul.txt: 0.218 -> 0.175 ms,
+// identical outputs); in the library the reference draw alone 0.068 -> 0.051 ms and
+// the reference-draw elem step 0.088 -> 0.071 ms (same-box A/B, r04n_ab_philox_mad.txt)
+__device__ __forceinline__ uint64_t mul_wide(uint32_t a, uint32_t b) {
+    uint64_t r;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "s"(a), "v"(b) : "vcc");
+    return r;
+}
+
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
-        const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
+        const uint64_t p0 = mul_wide(M0, c.x), p1 = mul_wide(M1, c.z);
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         // 3-input XORs as one gfx950 v_bitop3_b32 each (LUT 0x96 = a ^ b ^ c)
         c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k.x, 0x96), lo1,
                        __builtin_amdgcn_bitop3_b32(hi0, c.w, k.y, 0x96), lo0);
