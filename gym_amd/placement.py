@@ -99,7 +99,10 @@ class PlacedBuffer:
     def __init__(self, nbytes, device):
         dev = torch.device(device)
         self.device = dev
-        gran = granularity(dev)
+        # whole 2 MiB pages (the minimum granularity the driver reports is 4 KiB);
+        # see profiles/r04u_vmm_alias.txt for what is and is not safe with these
+        # allocations on this stack
+        gran = max(granularity(dev), self.ALIGN)
         self.nbytes = -(-int(nbytes) // gran) * gran
         hip = _hip()
         self.handle, self.va = ctypes.c_void_p(), ctypes.c_void_p()
@@ -177,3 +180,4 @@ def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac):
         if b is not best:
             b.release()
     return best, times
+

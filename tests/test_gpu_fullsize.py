@@ -10,6 +10,8 @@ properties that do not need the oracle to process the whole arena:
     tied), the residual delta matches, and the decode's sign step matches.
 Tolerances as in test_gpu_kernels.py (bit-exact for indices and same-order
 fp32 sums; 1e-6 relative for reordered fp32)."""
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -360,3 +362,52 @@ def test_placed_buffer_round_trip_and_diloco_placement():
     assert outs[0][3] is not None and outs[0][3]["candidates"] >= 2
     for a, b2 in zip(outs[0][:3], outs[1][:3]):
         assert torch.equal(a, b2)
+
+
+def test_replica_loop_placements_bit_exact_under_allocation_churn():
+    """The replica loop's two physical placements (the fused AdamW moments,
+    fused_optim.ArenaAdam._place; the DiLoCo master/momentum, DiLoCoOuter._place)
+    against the same loop with placement disabled, with ordinary allocations made,
+    written and freed between every step: every replica, the master, the momentum
+    and both moments bit-identical after each outer step
+    (tools/dbg_product_placement.py; profiles/r04u_vmm_alias.txt: hipMemCreate
+    allocations interleaved with ordinary ones were seen corrupted in other
+    patterns, so the product's pattern is pinned here)."""
+    from gym_amd import engine as E
+    from gym_amd import fused_optim as F
+    from gym_amd.arena import ReplicaArena
+    from gym_amd.comm import Collective
+    from gym_amd.fused_optim import ArenaAdam
+    torch.manual_seed(0)
+    base = torch.nn.Sequential(*[torch.nn.Linear(2048, 2048) for _ in range(3)]).to(DEV)  # 12.6M params
+
+    def run(placed):
+        oc, oa = E.PLACEMENT_CANDIDATES, F.PLACEMENT_CANDIDATES
+        if not placed:
+            E.PLACEMENT_CANDIDATES = F.PLACEMENT_CANDIDATES = 1
+        try:
+            ra = ReplicaArena([copy.deepcopy(base) for _ in range(4)])
+            opt = ArenaAdam(ra.params, ra, lr=1e-3, weight_decay=0.01)
+            eng = E.DiLoCoOuter(Collective(), 4, ra.ld, DEV, torch.float32)
+            eng.init_master(ra.flat_set[0])
+            g = torch.Generator(device=DEV)
+            g.manual_seed(5)
+            hist = []
+            for _ in range(3):
+                for _ in range(3):
+                    for p in ra.params:
+                        p.grad = torch.randn(p.shape, device=DEV, generator=g) * 1e-2
+                    opt.step()
+                    junk = [torch.empty(1 << 22, device=DEV).fill_(7.0) for _ in range(8)]
+                    del junk
+                eng(ra.flat_set)
+                hist.append([t.clone() for t in (ra.flat_set, eng.master, eng.mom, opt.M, opt.V)])
+            return hist, opt._placed is not None, eng.placement
+        finally:
+            E.PLACEMENT_CANDIDATES, F.PLACEMENT_CANDIDATES = oc, oa
+    a, adam_placed, dil = run(True)
+    b, _, _ = run(False)
+    assert dil is not None
+    for sa, sb in zip(a, b):
+        for x, y in zip(sa, sb):
+            assert torch.equal(x, y)
