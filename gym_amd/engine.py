@@ -199,7 +199,7 @@ class DiLoCoOuter:
         self.mom = self._state[self.per:] if momentum != 0 else None
         self.placement = None  # the placement probe's record (bench / DESIGN)
         self._placed_for = None
-        self._placed = None  # the PlacedBuffer holding the state, when one was chosen
+        self._placed = None  # the candidate buffer holding the state, when one was chosen
         self.first = True
         self.dtype = dtype
         self.sum = torch.empty(n, device=device, dtype=dtype) if (X and not self.shard) else None
@@ -234,8 +234,8 @@ class DiLoCoOuter:
         the replica set's make the step 1.88 instead of 1.57-1.65 ms at GPT-2
         124M x 8, and which one an allocation gets changes from process to
         process: the between-process spread of rounds 1-3).  So up to
-        PLACEMENT_CANDIDATES physical allocations (hipMemCreate, one at a time,
-        each mapped on its own) are timed once against the live replica set with
+        PLACEMENT_CANDIDATES fresh device allocations (one at a time, all held
+        until the choice) are timed once against the live replica set with
         ga_probe_diloco_placement -- the step's exact access pattern, every value
         written back unchanged -- beside the ordinary allocation; the fastest
         keeps the state, the others are released.  ~0.2 s once; at most
@@ -267,7 +267,7 @@ class DiLoCoOuter:
         del src
         torch.cuda.empty_cache()
         self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
-                          "how": "master+momentum in physical allocations (hipMemCreate) probed with the step's "
+                          "how": "master+momentum in fresh device allocations probed with the step's "
                                  "access pattern; candidate 0 = the ordinary allocation"}
 
     def __call__(self, reps):

@@ -99,7 +99,7 @@ class ArenaAdam(torch.optim.Optimizer):
             sp.sort(key=lambda t: t[1])
         self._partials = ops.sumsq_partials(dev, self.K)
         self._clip = torch.ones(2 * self.K, dtype=torch.float32, device=dev)
-        self._placed = None  # PlacedBuffer holding M and V once _place chose one
+        self._placed = None  # the candidate buffer holding M and V once _place chose one
         self.placement = None
 
     def _bind_state(self, p):
@@ -137,7 +137,7 @@ class ArenaAdam(torch.optim.Optimizer):
         step: the fused step's rate depends on where exp_avg / exp_avg_sq sit
         physically relative to the parameters and gradients (0.553-0.625 ms at
         GPT-2 124M, profiles/r04k_adam_placement.txt; gym_amd.placement), so up
-        to PLACEMENT_CANDIDATES physical allocations are timed with
+        to PLACEMENT_CANDIDATES fresh device allocations are timed with
         ga_probe_adam_placement (the step's access pattern, values unchanged)
         beside the ordinary ones and the fastest keeps the moments."""
         self._place_done = True

@@ -1,5 +1,6 @@
-"""Physically placed device buffers (HIP virtual memory management), for the
-state buffers the strategy step owns (DiLoCo master/momentum, AdamW moments).
+"""Physical placement of the state buffers the strategy step owns (DiLoCo
+master/momentum, AdamW moments): candidates probed with the step's own access
+pattern, the fastest kept.
 
 On MI355X the fused DiLoCo step runs 1.57-1.65 ms or 1.88 ms for the same
 virtual layout (GPT-2 124M x 8 replicas), depending on where its streams sit
@@ -12,13 +13,22 @@ share a class; tools/ubench_diloco_vmm.cpp, r04j: 1 GiB physical chunks created
 one by one fall in either class).  Which class a buffer gets is the driver's
 choice and differs between processes, so it cannot be fixed by a virtual layout.
 
-PlacedBuffer is one physical allocation (hipMemCreate) mapped at its own virtual
-range; engines create several, time the kernel's own access pattern on each
-(a probe that writes every value back unchanged), keep the fastest and release
-the rest.  The memory stays PyTorch-visible: `tensor()` wraps the mapping via
-__cuda_array_interface__ (the buffer owns it; keep the PlacedBuffer alive as
-long as the tensor is used).  This module only moves memory; every kernel stays
-behind the C ABI.
+The product's candidates are DeviceBuffer: fresh ordinary device allocations
+(each a new block of the caching allocator, i.e. its own hipMalloc), created
+one at a time and all held until the choice, so they land in different
+physical regions; engines time the kernel's own access pattern on each (a probe
+that writes every value back unchanged), keep the fastest and drop the rest.
+At GPT-2 124M x 8 the DiLoCo candidates fall in the 1.88 / 1.74 / 1.69 /
+1.76 ms classes and the chosen one runs the bench's step at 1.70 ms (frac
+0.731, profiles/r04w_*).
+
+PlacedBuffer -- one hipMemCreate allocation mapped at its own virtual range,
+wrapped via __cuda_array_interface__ -- is kept for the experiments under
+tools/ only: its candidates reach 1.65-1.66 ms, but on this stack such
+allocations were seen corrupted when interleaved with ordinary ones
+(profiles/r04u_vmm_alias.txt), and the product's bit-exact churn test failed
+with them once inside the full GPU suite.  This module only moves memory;
+every kernel stays behind the C ABI.
 """
 import ctypes
 import os
@@ -91,8 +101,9 @@ class _CAI:
 
 
 class PlacedBuffer:
-    """One physical allocation of `nbytes` (rounded up to the granularity)
-    mapped read-write at a virtual range of its own, on `device`."""
+    """One physical allocation of `nbytes` (rounded up to whole 2 MiB pages)
+    mapped read-write at a virtual range of its own, on `device`.  Experiments
+    only (tools/): not used by the product, see the module docstring."""
 
     ALIGN = 2 << 20  # virtual alignment of the mapping
 
@@ -143,6 +154,24 @@ class PlacedBuffer:
             pass
 
 
+class DeviceBuffer:
+    """One ordinary device allocation (the caching allocator's, i.e. hipMalloc
+    for a fresh block of this size) with PlacedBuffer's interface: the
+    candidates the product probes.  Held until the choice, so each candidate is
+    distinct memory; `release()` drops it (the caller empties the cache once)."""
+
+    def __init__(self, nbytes, device):
+        self.nbytes = -(-int(nbytes) // 16) * 16
+        self.device = torch.device(device)
+        self._t = torch.empty(self.nbytes, dtype=torch.uint8, device=self.device)
+
+    def tensor(self, dtype=torch.float32):
+        return self._t.view(dtype)
+
+    def release(self):
+        self._t = None
+
+
 def time_probe(fn, reps=3):
     """ms per call of fn (one warm-up, then reps calls between two events)."""
     fn()
@@ -155,26 +184,27 @@ def time_probe(fn, reps=3):
     return e0.elapsed_time(e1) / reps
 
 
-def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac):
-    """Create up to max_candidates - 1 physical allocations of nbytes one at a
-    time (all held until the choice is made, so each is distinct memory), time
-    probe(PlacedBuffer) on each, and return (the fastest PlacedBuffer, or None
-    when none beats baseline_ms -- the caller's ordinary allocation --, every
+def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=DeviceBuffer):
+    """Create up to max_candidates - 1 allocations of nbytes one at a time (all
+    held until the choice is made, so each is distinct memory; `kind` =
+    DeviceBuffer, ordinary allocations -- what the product uses -- or
+    PlacedBuffer), time probe(buffer) on each, and return (the fastest buffer, or
+    None when none beats baseline_ms -- the caller's own allocation --, every
     time in creation order with the baseline first).  At most max_frac of the
-    free device memory is taken; a device without virtual memory management, or
-    running out, ends the search with what was probed."""
+    free device memory is taken; running out ends the search with what was
+    probed."""
     times = [baseline_ms]
     best, best_t, held = None, baseline_ms, []
     budget = max_frac * torch.cuda.mem_get_info(torch.device(device))[0]
     try:
         while len(times) < max_candidates and (len(held) + 1) * nbytes <= budget:
-            buf = PlacedBuffer(nbytes, device)
+            buf = kind(nbytes, device)
             held.append(buf)
             t = probe(buf)
             times.append(t)
             if t < best_t:
                 best, best_t = buf, t
-    except RuntimeError:
+    except (RuntimeError, torch.cuda.OutOfMemoryError):
         pass
     for b in held:
         if b is not best:

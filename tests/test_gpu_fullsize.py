@@ -325,15 +325,15 @@ def test_sparta_reference_draw_gpt2_124m_32_nodes():
     assert torch.equal(outs[0][i, 0].cpu(), exp)
 
 
-def test_placed_buffer_round_trip_and_diloco_placement():
-    """gym_amd.placement: a physical allocation (hipMemCreate) mapped as a torch
-    tensor reads back what was written and is released; DiLoCoOuter's placement
-    probe leaves the replicas untouched and the outer step bit-identical to an
-    engine that kept its ordinary allocation."""
+def test_candidate_buffer_round_trip_and_diloco_placement():
+    """gym_amd.placement: a candidate buffer read as a torch tensor reads back
+    what was written and is released; DiLoCoOuter's placement probe leaves the
+    replicas untouched and the outer step bit-identical to an engine that kept
+    its ordinary allocation."""
     from gym_amd import engine as E
     from gym_amd.comm import Collective
-    from gym_amd.placement import PlacedBuffer
-    b = PlacedBuffer(3 << 20, DEV)
+    from gym_amd.placement import DeviceBuffer
+    b = DeviceBuffer(3 << 20, DEV)
     t = b.tensor()
     assert t.numel() * 4 >= 3 << 20 and t.is_cuda
     t.copy_(torch.arange(t.numel(), device=DEV, dtype=torch.float32))
