@@ -51,7 +51,7 @@ sys.path.insert(0, ROOT)
 from gym_amd import ops  # noqa: E402
 from gym_amd.arena import ArenaLayout, ReplicaSet  # noqa: E402
 from gym_amd.comm import Collective  # noqa: E402
-from gym_amd.engine import DeMoCodec, DiLoCoOuter, MeanReduce, Sparta  # noqa: E402
+from gym_amd.engine import DeMoCodec, DiLoCoOuter, MeanReduce, Sparta, place_demo_step  # noqa: E402
 from gym_amd.shapes import MODELS, numel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E, MI355X_MICROARCH.md
@@ -597,18 +597,7 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
     G = synth_replicas(layout, 1, coll.rank + 7, dev).data
     D = torch.zeros_like(P)
     codec = DeMoCodec(coll, 1, layout, dev)
-    te, td = KernelTimer(), KernelTimer()
-    codec.encode = te.wrap(codec.encode)
-    codec.decode = td.wrap(codec.decode)
-    te.on = td.on = True
-    t = timed_loop(lambda: codec(P, G, D, 1e-3, 0.999, 0.0), args.steps, args.warmup, coll)
     plan = codec.plan
-    flops_one = 0
-    for s in shapes:
-        from gym_amd.demo_codec import codec_view
-        R, C, n1, n2 = codec_view(s, 64)
-        flops_one += 2 * (R // n1) * (C // n2) * 2 * 64 ** 3  # two zero-padded 64^3 products per transform
-    enc_ms, dec_ms = te.mean_ms(), td.mean_ms()
     # the decode of 8 gathered payloads (what every GPU runs at 8 nodes): 8 nodes' own
     # payloads, each encoded from its own gradient (seeds 7..14) on the shared start,
     # so every chunk sees up to 8 * 32 distinct coefficients with 1-8 hitters each
@@ -621,6 +610,28 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
         Dk.zero_()
         ops.demo_encode(plan, P, Gk, Dk, gathered8[k:k + 1], 1e-3, 0.999, 1.0)
     del Gk, Dk
+    # the product's placement (the DeMo optimizer after its first step, probing with the
+    # payload it gathered: 8 sources at 8 nodes): G, P, D moved into the allocations the
+    # step runs fastest on
+    scratch = torch.empty_like(codec.payload)
+    placed, moved, placement = place_demo_step(
+        lambda p, g, d: ops.demo_encode(plan, p, g, d, scratch, 0.0, 0.999, 1.0),
+        lambda p, g: ops.demo_decode(plan, gathered8, p, g, 0.0), P, G, D)
+    del scratch
+    if placed is not None:
+        P, G, D = moved
+        placement["probed_with"] = "the 8-source payload"
+    te, td = KernelTimer(), KernelTimer()
+    codec.encode = te.wrap(codec.encode)
+    codec.decode = td.wrap(codec.decode)
+    te.on = td.on = True
+    t = timed_loop(lambda: codec(P, G, D, 1e-3, 0.999, 0.0), args.steps, args.warmup, coll)
+    flops_one = 0
+    for s in shapes:
+        from gym_amd.demo_codec import codec_view
+        R, C, n1, n2 = codec_view(s, 64)
+        flops_one += 2 * (R // n1) * (C // n2) * 2 * 64 ** 3  # two zero-padded 64^3 products per transform
+    enc_ms, dec_ms = te.mean_ms(), td.mean_ms()
     overlap = None
     if plan.M >= 32000:  # distinct (chunk, coefficient) hits over the 8 payloads, first 1000 chunks of wte
         e = torch.arange(32000, device=dev) // 32  # wte: 64x64 chunks, k = 32, chunk-local indices
@@ -698,7 +709,8 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
                         "non-temporal streams (the faster counts); frac = floor / encode time.  (The decode's "
                         "pattern probed this way ran slower than the 1-source decode itself, so it is no floor "
                         "and is not reported.)"},
-            "payload_entries": plan.M, "ref_bytes_tx": plan.reference_bytes(), "xgmi": xgmi}
+            "payload_entries": plan.M, "ref_bytes_tx": plan.reference_bytes(), "xgmi": xgmi,
+            "placement": placement}
 
 
 def bench_diloco_torch_gpu(args, coll, dev, fused_ms, model="gpt2-124m", K=8):

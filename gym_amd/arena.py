@@ -101,6 +101,7 @@ class ParamArena:
                 raise TypeError(f"ParamArena: mixed parameter dtypes ({p.dtype} vs {self.dtype})")
         self.layout = ArenaLayout([p.shape for p in self.params])
         n = self.layout.padded_to(world)
+        self.external = flat is not None
         if flat is not None:  # a row of a ReplicaArena (zeroed by its owner)
             if flat.numel() != n or (with_grad and (grad_flat is None or grad_flat.numel() != n)):
                 raise ValueError(f"ParamArena: external buffers must hold {n} elements")
@@ -155,6 +156,28 @@ class ParamArena:
         if self.grad_flat is not None:
             self.grad_flat.zero_()
             self.rebind_grads()
+
+    def relocate(self, flat, grad_flat):
+        """Move the parameters and gradients into new buffers of the same size
+        (contents copied; every parameter's .data and .grad re-pointed): how the
+        DeMo optimizer moves them into the memory its step runs fastest on."""
+        if self.external:
+            raise RuntimeError("ParamArena.relocate: the buffers belong to a ReplicaArena")
+        if flat.numel() != self.n or (self.grad_flat is not None and grad_flat.numel() != self.n):
+            raise ValueError("ParamArena.relocate: buffers of the arena's size")
+        with torch.no_grad():
+            if flat.data_ptr() != self.flat.data_ptr():
+                flat.copy_(self.flat)
+            self.flat = flat
+            for p, v in zip(self.params, self.layout.views(flat)):
+                p.data = v
+            self._data_ptrs = [p.data_ptr() for p in self.params]
+            if self.grad_flat is not None:
+                if grad_flat.data_ptr() != self.grad_flat.data_ptr():
+                    grad_flat.copy_(self.grad_flat)
+                self.grad_flat = grad_flat
+                self._grad_views = self.layout.views(grad_flat)
+                self.rebind_grads()
 
     def rebind_grads(self):
         """Point every trainable parameter's .grad back at its arena view."""

@@ -442,6 +442,15 @@ class DeMoCodec:
     def decode(self, P, G, lr):
         ops.demo_decode(self.plan, self.gathered, P, G, _f32(lr))
 
+    def place(self, P, G, D, decay=0.999):
+        """Placement of the step's parameters, gradient and delta (see
+        place_demo_step): the decode probed with this codec's last gathered
+        payload, the encode into a scratch payload."""
+        scratch = torch.empty_like(self.payload)
+        return place_demo_step(
+            lambda p, g, d: ops.demo_encode(self.plan, p, g, d, scratch, 0.0, _f32(decay), 1.0),
+            lambda p, g: ops.demo_decode(self.plan, self.gathered, p, g, 0.0), P, G, D)
+
     def __call__(self, P, G, D, lr, decay=0.999, weight_decay=0.0, all_gather=None):
         self.encode(P, G, D, lr, decay, weight_decay)
         self.exchange(all_gather)
@@ -452,6 +461,43 @@ import os as _os
 
 # tensor groups of the pipelined DeMo exchange (RCCL, world > 1); GA_DEMO_PIECES overrides
 DEMO_PIECES = int(_os.environ.get("GA_DEMO_PIECES", "2"))
+
+
+# DeMo step placement: fresh allocations probed per buffer
+DEMO_PLACEMENT_CANDIDATES = 32
+DEMO_PLACEMENT_MAX_FRAC = 0.3
+DEMO_PLACEMENT_MIN_BYTES = 64 << 20
+
+
+def place_demo_step(encode, decode, P, G, D):
+    """Where the DeMo step's parameters, gradient and delta sit physically sets
+    its rate the way master/momentum set the DiLoCo step's (GPT-2 350M 8-source
+    decode: 1.13 ms in ordinary allocations, 1.00 ms with either buffer in a
+    fast candidate, profiles/r04q_demo_decode_placement.txt).  `encode(P', G',
+    D')` and `decode(P', G')` are the step's kernels on any such buffers (the
+    decode at lr = 0 with the last gathered payload, the encode into a scratch
+    payload); gym_amd.placement.place_each probes up to
+    DEMO_PLACEMENT_CANDIDATES fresh allocations for G, then P, then D, each with
+    the others where they are by then, restores all three, and returns
+    ((buffer or None for P, G, D), (the P, G, D to use from now on), a record),
+    or (None, None, None) when the buffers are not worth it."""
+    from . import placement
+    if (P.device.type != "cuda" or not (P.shape == G.shape == D.shape)
+            or not (P.is_contiguous() and G.is_contiguous() and D.is_contiguous())
+            or 3 * P.numel() * P.element_size() < DEMO_PLACEMENT_MIN_BYTES or DEMO_PLACEMENT_CANDIDATES < 2):
+        return None, None, None
+
+    def run(g, p, d):
+        encode(p, g, d)
+        decode(p, g)
+    (bg, bp, bd), (g2, p2, d2), stages = placement.place_each([G, P, D], run, DEMO_PLACEMENT_CANDIDATES,
+                                                              DEMO_PLACEMENT_MAX_FRAC)
+    rec = {"what": "DeMo gradient, then parameters, then delta, each in the fresh device allocation the step's "
+                   "encode + decode run fastest on (probed with the others where they are by then)",
+           "ordinary_ms": round(stages[0], 4), "grad_placed_ms": round(stages[1], 4),
+           "param_placed_ms": round(stages[2], 4), "delta_placed_ms": round(stages[3], 4),
+           "placed": [b is not None for b in (bg, bp, bd)], "candidates_per_buffer": DEMO_PLACEMENT_CANDIDATES}
+    return (bp, bg, bd), (p2, g2, d2), rec
 
 
 def demo_codec(coll: Collective, K_local, layout, device, chunk=64, topk=32):
@@ -503,6 +549,19 @@ class PipelinedDeMoCodec:
 
     def reference_bytes(self, val_itemsize=4):
         return sum(c.plan.reference_bytes(val_itemsize) for c in self.codecs)
+
+    def place(self, P, G, D, decay=0.999):
+        """place_demo_step over every piece's encode and decode (each piece's last gathered payload)."""
+        scratch = [torch.empty_like(c.payload) for c in self.codecs]
+
+        def encode(p, g, d):
+            for c, sc in zip(self.codecs, scratch):
+                ops.demo_encode(c.plan, p, g, d, sc, 0.0, _f32(decay), 1.0)
+
+        def decode(p, g):
+            for c in self.codecs:
+                ops.demo_decode(c.plan, c.gathered, p, g, 0.0)
+        return place_demo_step(encode, decode, P, G, D)
 
     def __call__(self, P, G, D, lr, decay=0.999, weight_decay=0.0):
         pending = []

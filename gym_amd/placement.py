@@ -211,3 +211,46 @@ def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=De
             b.release()
     return best, times
 
+
+
+def place_each(tensors, run, max_candidates, max_frac, reps=3):
+    """Placement for buffers a step streams together (the DeMo step's gradient,
+    parameters and delta), one buffer at a time: `run(*ts)` launches the step's
+    kernels on any buffers of these shapes.  The buffers are snapshotted and the
+    ordinary set timed; then for each buffer in turn up to max_candidates fresh
+    allocations are probed with the others where they are by then (moved or
+    not), and the fastest is kept when it beats the set's best time so far.
+    Every buffer is restored from the snapshot (the probe may write what it
+    likes) and each moved one receives its contents.  Returns (per buffer: its
+    candidate buffer or None, per buffer: the tensor to use from now on, the
+    stage times: ordinary set first)."""
+    for t in tensors:
+        if not t.is_contiguous():
+            raise ValueError("place_each: contiguous buffers")
+    saved = [t.clone() for t in tensors]
+    cur = list(tensors)
+    placed = [None] * len(tensors)
+
+    def view(buf, i):
+        return buf.tensor(tensors[i].dtype)[:tensors[i].numel()].view(tensors[i].shape)
+
+    best_t = time_probe(lambda: run(*cur), reps)
+    stages = [best_t]
+    for i, t in enumerate(tensors):
+        def probe(buf, i=i):
+            c = view(buf, i)
+            c.copy_(saved[i])
+            args = list(cur)
+            args[i] = c
+            return time_probe(lambda: run(*args), reps)
+        best, times = choose(t.numel() * t.element_size(), t.device, probe, best_t, max_candidates, max_frac)
+        if best is not None:
+            placed[i], cur[i] = best, view(best, i)
+            best_t = min(times)
+        stages.append(min(times))
+        torch.cuda.empty_cache()
+    for t, c, sv in zip(tensors, cur, saved):
+        t.copy_(sv)
+        if c is not t:
+            c.copy_(sv)
+    return placed, cur, stages

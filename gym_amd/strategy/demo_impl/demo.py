@@ -75,9 +75,25 @@ class DeMo(torch.optim.SGD):
         self.demo_state = {}
         for p, d in zip(trainable, self.arena.layout.views(self.delta_flat)):
             self.demo_state[p] = {"step": 0, "delta": d}
+        self.placement, self._placed = None, None
         itemsize = torch.finfo(self.default_dtype).bits // 8
         ref = self.codec.reference_bytes if isinstance(self.codec, PipelinedDeMoCodec) else self.codec.plan.reference_bytes
         self._tx = ref(itemsize)
+
+    def _place(self, P, G, D):
+        """Once, after the first step: move the gradient, parameter and delta
+        arenas into the device allocations the step's kernels run fastest on
+        (engine.place_demo_step; the probe decodes at lr = 0, encodes into a
+        scratch payload and restores P, G and D, so the results are unchanged)."""
+        bufs, tens, rec = self.codec.place(P, G, D, self.compression_decay)
+        self.placement = rec or {"placed": False}
+        if bufs is not None and any(b is not None for b in bufs):
+            self.arena.relocate(tens[0].view(-1), tens[1].view(-1))
+            if tens[2].data_ptr() != self.delta_flat.data_ptr():
+                self.delta_flat = tens[2].view(-1)
+                for st, d in zip(self.demo_state.values(), self.arena.layout.views(self.delta_flat)):
+                    st["delta"] = d
+            self._placed = bufs  # own the memory the parameters / gradients / deltas now live in
 
     def _gather_fn(self):
         from ..communicate import all_gather as ours
@@ -107,6 +123,8 @@ class DeMo(torch.optim.SGD):
             self.codec.encode(P, G, D, lr, self.compression_decay, self.weight_decay)
             self.codec.exchange(self._gather_fn())
             self.codec.decode(P, G, lr)
+        if self.placement is None:
+            self._place(P, G, D)
         self.data_transmit = self._tx
         self.data_receive = self._tx * self.coll.world
         return loss

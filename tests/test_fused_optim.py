@@ -91,3 +91,33 @@ def test_arena_adam_state_dict_round_trip(fake, source):
     # the state the optimizer reports is the state the kernel uses
     p0 = next(a.parameters())
     assert opt.state[p0]["exp_avg"].data_ptr() == opt.M.data_ptr()
+
+
+def test_param_arena_relocate_moves_params_and_grads():
+    """ParamArena.relocate (the DeMo optimizer's move into the memory its step runs
+    fastest on): contents copied, every parameter's .data and .grad re-pointed into
+    the new buffers, autograd accumulating there afterwards; a ReplicaArena row
+    refuses."""
+    from gym_amd.arena import ParamArena
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(5, 3), torch.nn.Linear(3, 2))
+    a = ParamArena(list(m.parameters()))
+    x = torch.randn(4, 5)
+    m(x).sum().backward()
+    before = [p.detach().clone() for p in m.parameters()]
+    grads = [p.grad.clone() for p in m.parameters()]
+    flat, gflat = torch.full((a.n,), 7.0), torch.full((a.n,), 7.0)
+    a.relocate(flat, gflat)
+    a.check_bound()
+    assert a.flat is flat and a.grad_flat is gflat
+    for p, b, g, v, gv in zip(m.parameters(), before, grads, a.layout.views(flat), a.layout.views(gflat)):
+        assert torch.equal(p.detach(), b) and p.data_ptr() == v.data_ptr()
+        assert torch.equal(p.grad, g) and p.grad.data_ptr() == gv.data_ptr()
+    m(x).sum().backward()  # accumulates into the relocated grad views
+    for p, g in zip(m.parameters(), grads):
+        assert torch.allclose(p.grad, 2 * g)
+    lin = list(torch.nn.Linear(2, 2).parameters())
+    n = ParamArena([torch.nn.Parameter(q.detach().clone()) for q in lin]).n
+    ext = ParamArena(lin, flat=torch.zeros(n), with_grad=False)
+    with pytest.raises(RuntimeError):
+        ext.relocate(torch.zeros(ext.n), None)

@@ -411,3 +411,54 @@ def test_replica_loop_placements_bit_exact_under_allocation_churn():
     for sa, sb in zip(a, b):
         for x, y in zip(sa, sb):
             assert torch.equal(x, y)
+
+
+def test_demo_step_placement_leaves_the_step_unchanged():
+    """The DeMo optimizer moves its gradient, parameter and delta arenas into the
+    device allocations its step runs fastest on, once, after the first step
+    (engine.place_demo_step): the probe decodes at lr = 0, encodes into a scratch
+    payload and restores P, G and D, so three steps give bit-identical parameters
+    to an optimizer that kept its ordinary allocations, and after the move the
+    parameters, their .grad (autograd still writes it) and the deltas live in
+    the chosen buffers."""
+    from gym_amd import engine as E
+    from gym_amd.strategy.demo_impl.demo import DeMo
+    torch.manual_seed(0)
+    base = torch.nn.Sequential(*[torch.nn.Linear(2048, 2048) for _ in range(3)]).to(DEV)  # 12.6M params
+    x = torch.randn(64, 2048, device=DEV)
+    # fixed per-step gradients (the backward's GEMMs may pick other kernels for other
+    # addresses; the step under test is the optimizer's)
+    grads = [[torch.randn_like(p) * 1e-2 for p in base.parameters()] for _ in range(3)]
+    outs = []
+    for min_bytes in (E.DEMO_PLACEMENT_MIN_BYTES, 1 << 62):
+        old = E.DEMO_PLACEMENT_MIN_BYTES
+        E.DEMO_PLACEMENT_MIN_BYTES = min_bytes
+        try:
+            model = copy.deepcopy(base)
+            opt = DeMo(model.parameters(), lr=1e-3, compression_topk=32, compression_chunk=64)
+            for s in range(3):
+                opt.zero_grad()
+                model(x).square().mean().backward()  # autograd writes .grad (in the moved arena after step 1)
+                for p, g in zip(model.parameters(), grads[s]):
+                    p.grad.copy_(g)
+                opt.step()
+            outs.append(([p.detach().clone() for p in model.parameters()], opt))
+        finally:
+            E.DEMO_PLACEMENT_MIN_BYTES = old
+    opt = outs[0][1]
+    assert opt.placement is not None and "grad_placed_ms" in opt.placement
+    assert outs[1][1].placement == {"placed": False}
+
+    def inside(buf, ptr):
+        if buf is None:
+            return False
+        t = buf.tensor(torch.uint8)
+        return t.data_ptr() <= ptr < t.data_ptr() + t.numel()
+    if opt._placed is not None:
+        bp, bg, bd = opt._placed
+        for p in opt.arena.params:
+            assert inside(bp, p.data_ptr()) == (bp is not None)
+            assert inside(bg, p.grad.data_ptr()) == (bg is not None)
+            assert inside(bd, opt.demo_state[p]["delta"].data_ptr()) == (bd is not None)
+    for a, b in zip(outs[0][0], outs[1][0]):
+        assert torch.equal(a, b)
