@@ -615,7 +615,7 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
     # step runs fastest on
     scratch = torch.empty_like(codec.payload)
     placed, moved, placement = place_demo_step(
-        lambda p, g, d: ops.demo_encode(plan, p, g, d, scratch, 0.0, 0.999, 1.0),
+        lambda p, g, d: ops.demo_encode(plan, p, g, d, scratch, 1e-3, 0.999, 1.0),
         lambda p, g: ops.demo_decode(plan, gathered8, p, g, 0.0), P, G, D)
     del scratch
     if placed is not None:

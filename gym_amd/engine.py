@@ -442,13 +442,14 @@ class DeMoCodec:
     def decode(self, P, G, lr):
         ops.demo_decode(self.plan, self.gathered, P, G, _f32(lr))
 
-    def place(self, P, G, D, decay=0.999):
+    def place(self, P, G, D, lr, decay=0.999):
         """Placement of the step's parameters, gradient and delta (see
         place_demo_step): the decode probed with this codec's last gathered
-        payload, the encode into a scratch payload."""
+        payload, the encode (the step's lr and decay: the chunks take the same
+        top-k path as in the step) into a scratch payload."""
         scratch = torch.empty_like(self.payload)
         return place_demo_step(
-            lambda p, g, d: ops.demo_encode(self.plan, p, g, d, scratch, 0.0, _f32(decay), 1.0),
+            lambda p, g, d: ops.demo_encode(self.plan, p, g, d, scratch, _f32(lr), _f32(decay), 1.0),
             lambda p, g: ops.demo_decode(self.plan, self.gathered, p, g, 0.0), P, G, D)
 
     def __call__(self, P, G, D, lr, decay=0.999, weight_decay=0.0, all_gather=None):
@@ -475,8 +476,8 @@ def place_demo_step(encode, decode, P, G, D):
     decode: 1.13 ms in ordinary allocations, 1.00 ms with either buffer in a
     fast candidate, profiles/r04q_demo_decode_placement.txt).  `encode(P', G',
     D')` and `decode(P', G')` are the step's kernels on any such buffers (the
-    decode at lr = 0 with the last gathered payload, the encode into a scratch
-    payload); gym_amd.placement.place_each probes up to
+    decode at lr = 0 with the last gathered payload, the encode with the step's
+    lr into a scratch payload); gym_amd.placement.place_each probes up to
     DEMO_PLACEMENT_CANDIDATES fresh allocations for G, then P, then D, each with
     the others where they are by then, restores all three, and returns
     ((buffer or None for P, G, D), (the P, G, D to use from now on), a record),
@@ -550,13 +551,13 @@ class PipelinedDeMoCodec:
     def reference_bytes(self, val_itemsize=4):
         return sum(c.plan.reference_bytes(val_itemsize) for c in self.codecs)
 
-    def place(self, P, G, D, decay=0.999):
+    def place(self, P, G, D, lr, decay=0.999):
         """place_demo_step over every piece's encode and decode (each piece's last gathered payload)."""
         scratch = [torch.empty_like(c.payload) for c in self.codecs]
 
         def encode(p, g, d):
             for c, sc in zip(self.codecs, scratch):
-                ops.demo_encode(c.plan, p, g, d, sc, 0.0, _f32(decay), 1.0)
+                ops.demo_encode(c.plan, p, g, d, sc, _f32(lr), _f32(decay), 1.0)
 
         def decode(p, g):
             for c in self.codecs:

@@ -80,12 +80,12 @@ class DeMo(torch.optim.SGD):
         ref = self.codec.reference_bytes if isinstance(self.codec, PipelinedDeMoCodec) else self.codec.plan.reference_bytes
         self._tx = ref(itemsize)
 
-    def _place(self, P, G, D):
+    def _place(self, P, G, D, lr):
         """Once, after the first step: move the gradient, parameter and delta
         arenas into the device allocations the step's kernels run fastest on
         (engine.place_demo_step; the probe decodes at lr = 0, encodes into a
         scratch payload and restores P, G and D, so the results are unchanged)."""
-        bufs, tens, rec = self.codec.place(P, G, D, self.compression_decay)
+        bufs, tens, rec = self.codec.place(P, G, D, lr, self.compression_decay)
         self.placement = rec or {"placed": False}
         if bufs is not None and any(b is not None for b in bufs):
             self.arena.relocate(tens[0].view(-1), tens[1].view(-1))
@@ -124,7 +124,7 @@ class DeMo(torch.optim.SGD):
             self.codec.exchange(self._gather_fn())
             self.codec.decode(P, G, lr)
         if self.placement is None:
-            self._place(P, G, D)
+            self._place(P, G, D, lr)
         self.data_transmit = self._tx
         self.data_receive = self._tx * self.coll.world
         return loss
