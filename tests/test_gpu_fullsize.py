@@ -462,3 +462,39 @@ def test_demo_step_placement_leaves_the_step_unchanged():
             assert inside(bd, opt.demo_state[p]["delta"].data_ptr()) == (bd is not None)
     for a, b in zip(outs[0][0], outs[1][0]):
         assert torch.equal(a, b)
+
+
+def test_pipelined_demo_codec_placement_restores_and_matches():
+    """PipelinedDeMoCodec.place (the multi-GPU DeMo codec's placement; here over
+    two tensor groups without an exchange): P, G, D come back bit-identical, the
+    moved buffers hold the same contents, and the next step on them equals the
+    step on the ordinary buffers."""
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.comm import Collective
+    from gym_amd.engine import PipelinedDeMoCodec
+    shapes = [(2048, 2048), (2048,), (4096, 1024), (1024,)] * 2
+    layout = ArenaLayout(shapes)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    n = layout.n
+    P = (torch.randn(1, n, device=DEV, generator=g) * 0.02)
+    G = torch.randn(1, n, device=DEV, generator=g) * 1e-3
+    D = torch.zeros(1, n, device=DEV)
+    codec = PipelinedDeMoCodec(Collective(), 1, layout, DEV, pieces=2)
+    assert len(codec.codecs) == 2
+    codec(P, G, D, 1e-3)
+    snap = [t.clone() for t in (P, G, D)]
+    bufs, moved, rec = codec.place(P, G, D, 1e-3)
+    assert rec is not None and len(rec["placed"]) == 3
+    for t, s in zip((P, G, D), snap):
+        assert torch.equal(t, s)
+    for t, s in zip(moved, snap):
+        assert torch.equal(t, s)
+    G2 = torch.randn(1, n, device=DEV, generator=g) * 1e-3
+    P1, G1, D1 = P.clone(), G2.clone(), D.clone()
+    Pm, Gm, Dm = moved
+    Gm.copy_(G2)
+    codec(P1, G1, D1, 1e-3)
+    codec(Pm, Gm, Dm, 1e-3)
+    for a, b in zip((P1, G1, D1), (Pm, Gm, Dm)):
+        assert torch.equal(a, b)
