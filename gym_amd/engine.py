@@ -491,8 +491,12 @@ def place_demo_step(encode, decode, P, G, D):
     def run(g, p, d):
         encode(p, g, d)
         decode(p, g)
-    (bg, bp, bd), (g2, p2, d2), stages = placement.place_each([G, P, D], run, DEMO_PLACEMENT_CANDIDATES,
-                                                              DEMO_PLACEMENT_MAX_FRAC)
+    try:  # only the snapshots can run out of memory before anything is touched (candidates: choose)
+        (bg, bp, bd), (g2, p2, d2), stages = placement.place_each([G, P, D], run, DEMO_PLACEMENT_CANDIDATES,
+                                                                  DEMO_PLACEMENT_MAX_FRAC)
+    except torch.cuda.OutOfMemoryError:
+        torch.cuda.empty_cache()
+        return None, None, {"placed": False, "why": "no memory for the snapshots"}
     rec = {"what": "DeMo gradient, then parameters, then delta, each in the fresh device allocation the step's "
                    "encode + decode run fastest on (probed with the others where they are by then)",
            "ordinary_ms": round(stages[0], 4), "grad_placed_ms": round(stages[1], 4),

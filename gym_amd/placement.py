@@ -227,7 +227,7 @@ def place_each(tensors, run, max_candidates, max_frac, reps=3):
     for t in tensors:
         if not t.is_contiguous():
             raise ValueError("place_each: contiguous buffers")
-    saved = [t.clone() for t in tensors]
+    saved = [t.clone() for t in tensors]  # the only allocation before the buffers are touched
     cur = list(tensors)
     placed = [None] * len(tensors)
 

@@ -87,7 +87,7 @@ class DeMo(torch.optim.SGD):
         scratch payload and restores P, G and D, so the results are unchanged)."""
         bufs, tens, rec = self.codec.place(P, G, D, lr, self.compression_decay)
         self.placement = rec or {"placed": False}
-        if bufs is not None and any(b is not None for b in bufs):
+        if bufs is not None and tens is not None and any(b is not None for b in bufs):
             self.arena.relocate(tens[0].view(-1), tens[1].view(-1))
             if tens[2].data_ptr() != self.delta_flat.data_ptr():
                 self.delta_flat = tens[2].view(-1)
