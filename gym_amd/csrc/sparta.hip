@@ -638,6 +638,60 @@ struct WaveBatchDpp {
     }
 };
 
+// WaveBatchDpp with each lane holding TWO 4-replica vectors (32 contiguous bytes
+// of the element's line): KQ / 2 lanes per element, 128 / KQ elements per pass,
+// the ascending-replica walk KQ / 2 steps of 8 adds.  Same sum order as
+// WaveBatchDpp (bit-identical); half the walk steps per element, so ~20 listed
+// elements take two passes of 4 steps instead of three of 8.
+template <typename T, int KQ>
+struct WaveBatchDpp2 {
+    static constexpr int LQ = KQ / 2, K = 4 * KQ, EPP = 64 / LQ, NP = 4, EB = NP * EPP;
+    using V = typename Vec4<T>::type;
+    __device__ __forceinline__ static float shr1(float a) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x111, 0xf, 0xf, true));
+    }
+    __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0,
+                                               int ne, int lane, float divisor) {
+        const int q = lane % LQ, el = lane / LQ;
+        V v[NP][2];
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int e = u * EPP + el;
+            if (e < ne) {
+                const V* p = reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 8 * q);
+                v[u][0] = stream_load(p);
+                v[u][1] = stream_load(p + 1);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            if (u * EPP >= ne) break;  // wave-uniform
+            const int e = u * EPP + el;
+            float f0[4] = {0.f, 0.f, 0.f, 0.f}, f1[4] = {0.f, 0.f, 0.f, 0.f};
+            if (e < ne) {
+                Vec4<T>::unpack(v[u][0], f0);
+                Vec4<T>::unpack(v[u][1], f1);
+            }
+            const float f[8] = {f0[0], f0[1], f0[2], f0[3], f1[0], f1[1], f1[2], f1[3]};
+            float a = 0.f;
+#pragma unroll
+            for (int s = 0; s < LQ; ++s) {
+                float left = LQ > 1 ? shr1(a) : 0.f;
+                if (q == 0) left = 0.f;
+                const float c = (((((((left + f[0]) + f[1]) + f[2]) + f[3]) + f[4]) + f[5]) + f[6]) + f[7];
+                a = q == s ? c : a;
+            }
+            const float avg = __shfl(a / divisor, (lane & ~(LQ - 1)) | (LQ - 1), 64);
+            if (e < ne) {
+                const float w[4] = {avg, avg, avg, avg};
+                V* p = reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 8 * q);
+                stream_store(p, Vec4<T>::pack(w));
+                stream_store(p + 1, Vec4<T>::pack(w));
+            }
+        }
+    }
+};
+
 // 8 waves per SIMD: the per-source instantiations fit 64 VGPRs without spills
 // (67 / 63 unconstrained); Philox mode 0.048 -> 0.045 ms, reference draw
 // unchanged (profiles/r02z_ab_sparta_split_wpe.txt)
@@ -688,8 +742,19 @@ __global__ __launch_bounds__(64 * kSpWaves) GA_SP_WPE_ATTR void sparta_average_w
         }
         wave_sync();
         const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
-        for (int b0 = 0; b0 < wtot; b0 += B::EB)
-            B::run(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, divisor);
+        // the reference draw leaves the kernel VALU-bound: the two-vector batch's shorter
+        // walk takes it 0.0717 -> 0.0664 ms; the Philox stream's memory-bound step runs
+        // 0.042 -> 0.048 ms with it, so that keeps the one-vector batch
+        // (profiles/r04ac_ab_sparta_dpp2.txt)
+        if (KQ >= 2 && SRC == 1) {
+            using B2 = WaveBatchDpp2<T, (KQ >= 2 ? KQ : 2)>;
+            for (int b0 = 0; b0 < wtot; b0 += B2::EB)
+                B2::run(src, ld, tile0, list, b0, (wtot - b0) < B2::EB ? (wtot - b0) : B2::EB, lane, divisor);
+        } else {
+            for (int b0 = 0; b0 < wtot; b0 += B::EB)
+                B::run(src, ld, tile0, list, b0, (wtot - b0) < B::EB ? (wtot - b0) : B::EB, lane, divisor);
+        }
+        wave_sync();  // the list is rewritten by the next window
     }
 }
 
