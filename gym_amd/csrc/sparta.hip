@@ -638,14 +638,16 @@ struct WaveBatchDpp {
     }
 };
 
-// WaveBatchDpp with each lane holding TWO 4-replica vectors (32 contiguous bytes
-// of the element's line): KQ / 2 lanes per element, 128 / KQ elements per pass,
-// the ascending-replica walk KQ / 2 steps of 8 adds.  Same sum order as
-// WaveBatchDpp (bit-identical); half the walk steps per element, so ~20 listed
-// elements take two passes of 4 steps instead of three of 8.
-template <typename T, int KQ>
+// WaveBatchDpp with each lane holding VPL 4-replica vectors (16 VPL contiguous
+// bytes of the element's line): KQ / VPL lanes per element, 64 VPL / KQ elements
+// per pass, the ascending-replica walk KQ / VPL steps of 4 VPL adds.  Same sum
+// order as WaveBatchDpp (bit-identical); 1 / VPL of the walk steps per element,
+// so ~20 listed elements take two passes of 4 steps instead of three of 8 at
+// VPL = 2.
+constexpr int kSpVpl = 2;  // 4 vectors per lane: 0.0667 -> 0.072 ms (profiles/r04ad_ab_sparta_vpl4.txt)
+template <typename T, int KQ, int VPL = kSpVpl>
 struct WaveBatchDpp2 {
-    static constexpr int LQ = KQ / 2, K = 4 * KQ, EPP = 64 / LQ, NP = 4, EB = NP * EPP;
+    static constexpr int LQ = KQ / VPL, K = 4 * KQ, EPP = 64 / LQ, NP = 8 / VPL, EB = NP * EPP;
     using V = typename Vec4<T>::type;
     __device__ __forceinline__ static float shr1(float a) {
         return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x111, 0xf, 0xf, true));
@@ -653,40 +655,41 @@ struct WaveBatchDpp2 {
     __device__ __forceinline__ static void run(T* src, int64_t ld, int64_t tile0, const uint16_t* list, int b0,
                                                int ne, int lane, float divisor) {
         const int q = lane % LQ, el = lane / LQ;
-        V v[NP][2];
+        V v[NP][VPL];
 #pragma unroll
         for (int u = 0; u < NP; ++u) {
             const int e = u * EPP + el;
             if (e < ne) {
-                const V* p = reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 8 * q);
-                v[u][0] = stream_load(p);
-                v[u][1] = stream_load(p + 1);
+                const V* p = reinterpret_cast<const V*>(src + (tile0 + list[b0 + e]) * ld + 4 * VPL * q);
+#pragma unroll
+                for (int j = 0; j < VPL; ++j) v[u][j] = stream_load(p + j);
             }
         }
 #pragma unroll
         for (int u = 0; u < NP; ++u) {
             if (u * EPP >= ne) break;  // wave-uniform
             const int e = u * EPP + el;
-            float f0[4] = {0.f, 0.f, 0.f, 0.f}, f1[4] = {0.f, 0.f, 0.f, 0.f};
-            if (e < ne) {
-                Vec4<T>::unpack(v[u][0], f0);
-                Vec4<T>::unpack(v[u][1], f1);
+            float f[VPL][4];
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) {
+                f[j][0] = f[j][1] = f[j][2] = f[j][3] = 0.f;
+                if (e < ne) Vec4<T>::unpack(v[u][j], f[j]);
             }
-            const float f[8] = {f0[0], f0[1], f0[2], f0[3], f1[0], f1[1], f1[2], f1[3]};
             float a = 0.f;
 #pragma unroll
             for (int s = 0; s < LQ; ++s) {
-                float left = LQ > 1 ? shr1(a) : 0.f;
-                if (q == 0) left = 0.f;
-                const float c = (((((((left + f[0]) + f[1]) + f[2]) + f[3]) + f[4]) + f[5]) + f[6]) + f[7];
+                float c = LQ > 1 ? shr1(a) : 0.f;
+                if (q == 0) c = 0.f;
+#pragma unroll
+                for (int j = 0; j < VPL; ++j) c = (((c + f[j][0]) + f[j][1]) + f[j][2]) + f[j][3];
                 a = q == s ? c : a;
             }
             const float avg = __shfl(a / divisor, (lane & ~(LQ - 1)) | (LQ - 1), 64);
             if (e < ne) {
                 const float w[4] = {avg, avg, avg, avg};
-                V* p = reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 8 * q);
-                stream_store(p, Vec4<T>::pack(w));
-                stream_store(p + 1, Vec4<T>::pack(w));
+                V* p = reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 4 * VPL * q);
+#pragma unroll
+                for (int j = 0; j < VPL; ++j) stream_store(p + j, Vec4<T>::pack(w));
             }
         }
     }
@@ -746,8 +749,8 @@ __global__ __launch_bounds__(64 * kSpWaves) GA_SP_WPE_ATTR void sparta_average_w
         // walk takes it 0.0717 -> 0.0664 ms; the Philox stream's memory-bound step runs
         // 0.042 -> 0.048 ms with it, so that keeps the one-vector batch
         // (profiles/r04ac_ab_sparta_dpp2.txt)
-        if (KQ >= 2 && SRC == 1) {
-            using B2 = WaveBatchDpp2<T, (KQ >= 2 ? KQ : 2)>;
+        if (KQ >= kSpVpl && SRC == 1) {
+            using B2 = WaveBatchDpp2<T, (KQ >= kSpVpl ? KQ : kSpVpl)>;
             for (int b0 = 0; b0 < wtot; b0 += B2::EB)
                 B2::run(src, ld, tile0, list, b0, (wtot - b0) < B2::EB ? (wtot - b0) : B2::EB, lane, divisor);
         } else {
