@@ -16,13 +16,13 @@ roofline = the fused ga_diloco_outer kernel: algorithmic HBM bytes per launch
         = HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE x2 on
         gfx950, WRITE_SIZE) of this same configuration, run by this script as
         child processes before it touches the GPU itself; "copy_GBps" = a
-        float4 streaming copy (ga_stream_copy) timed in this process, what the
-        box streams.
+        float4 streaming copy (ga_stream_copy) between two ordinary
+        allocations timed in this process, what the box streams unplaced.
 cpu_baseline = the reference's DiLoCo outer step restated per tensor in torch
         (oracle/torch_diloco.py, bit-exact with the reference's golden run),
         over gloo with 8 node processes x (cores/8) threads on this host, on
-        the full GPT-2 124M parameter list, N=1 only, run before the GPU is
-        initialised.
+        the full GPT-2 124M parameter list (configs[2]: 8 nodes), run on
+        rank 0 before the GPU is initialised; at N > 1 the same 8-node job.
 
 Extra lines in "extras" (same timing rules, not the headline): SPARTA (32
 nodes in total, 32/G per GPU, p=0.005, Philox mask: configs[3]), SimpleReduce
@@ -34,6 +34,11 @@ reduce-scatter/all-gather over xGMI dominates (its "xgmi" block).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-extras]
        torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+`python bench.py --gpus N` with N > 1 and no torchrun environment launches
+itself: this process runs the host legs (the CPU baseline) without touching
+the GPU, starts `python -m torch.distributed.run --nproc-per-node N bench.py`
+as a child process (one rank per GPU), and prints rank 0's JSON line with
+the CPU baseline merged in (self_launch below).
 """
 import argparse
 import json
@@ -353,10 +358,10 @@ def bench_diloco(args, coll, dev):
             "kernel_ms_single_launch_events": round(kern_single, 4) if kern_single is not None else None,
             "sustained": {"launches": SUSTAINED_LAUNCHES, "kernel_ms": round(sus_ms, 4),
                           "frac": round(alg_bytes / (sus_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                          "copy_GBps": round(copy_sus, 1),
-                          "frac_of_copy": round(alg_bytes / (sus_ms * 1e-3) / 1e9 / copy_sus, 4)} if sus_ms else None,
+                          "copy_GBps": round(copy_sus, 1)} if sus_ms else None,
+            # a float4 copy between two ordinary allocations in this process: what the box
+            # streams without placement (the placed kernel can exceed it, so no ratio is given)
             "copy_GBps": round(copy, 1) if copy else None,
-            "frac_of_copy": round(achieved / copy, 4) if copy else None,
             # master/momentum placement chosen by DiLoCoOuter._place (probe times per candidate)
             "placement": eng.placement},
     }
@@ -789,6 +794,73 @@ def bench_inner_adamw(args, coll, dev, model="gpt2-124m", max_norm=1.0):
                                                      opt.placement["probe_ms"][0]] if opt.placement else None)}
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def child_command(argv, gpus, port):
+    """The torch.distributed.run command of a self-launched N-rank bench: one
+    rank per GPU on this node, 127.0.0.1 rendezvous, the parent's arguments
+    passed on (the host legs already ran in the parent: --no-cpu-baseline)."""
+    rest = [a for a in argv if a != "--no-cpu-baseline"]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.join(ROOT, "bench.py"), *rest, "--no-cpu-baseline"]
+
+
+def merge_child_line(stdout_text, cpu, legs, cmd):
+    """Rank 0's one JSON line from the child's stdout, with the parent's CPU
+    baseline and host legs merged in; None when the child printed none."""
+    line = None
+    for raw in stdout_text.splitlines():
+        raw = raw.strip()
+        if raw.startswith("{") and '"metric"' in raw:
+            try:
+                line = json.loads(raw)
+            except ValueError:
+                continue
+    if line is None:
+        return None
+    line["cpu_baseline"] = cpu
+    hl = dict(line.get("host_legs_s") or {})
+    hl.update({f"parent_{k}": v for k, v in legs.items()})
+    line["host_legs_s"] = hl
+    line["launch"] = ("self-launched: this process ran the host legs without touching the GPU, then "
+                      f"`{' '.join(os.path.basename(c) if c == sys.executable else c for c in cmd[1:7])} ...` "
+                      "as a child process; rank 0's line")
+    return line
+
+
+def self_launch(args, argv):
+    """`bench.py --gpus N` (N > 1) outside torchrun: host legs here, N ranks in a
+    fresh torch.distributed.run child (this process never initialises the GPU,
+    so nothing execs from a GPU-initialised process).  Returns the exit code."""
+    import subprocess
+    legs = {}
+    t0 = time.perf_counter()
+    cpu = None
+    if not args.no_cpu_baseline and args.only is None:
+        cpu = cpu_baseline_diloco(args.model, args.replicas)
+    legs["cpu_baseline_s"] = round(time.perf_counter() - t0, 1)
+    cmd = child_command(argv, args.gpus, free_port())
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this pool
+    print(f"[bench] self-launch: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    line = merge_child_line(r.stdout, cpu, legs, cmd)
+    if line is None:
+        sys.stderr.write(r.stdout[-4000:])
+        print(f"[bench] the {args.gpus}-rank child printed no JSON line (rc {r.returncode})", file=sys.stderr)
+        return r.returncode or 1
+    print(json.dumps(line), flush=True)
+    return r.returncode
+
+
 def main():
     t_start = time.perf_counter()
     ap = argparse.ArgumentParser()
@@ -809,7 +881,10 @@ def main():
     if os.environ.get("GA_BENCH_WATCHDOG"):  # debugging aid: Python stacks on stderr every N s
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["GA_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
+    if args.gpus > 1 and "RANK" not in os.environ and not args.pmc_child:
+        sys.exit(self_launch(args, sys.argv[1:]))
     single = args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    rank0 = int(os.environ.get("RANK", "0")) == 0
     if args.pmc_child:  # a rocprofv3 PMC pass: the headline kernel only, a few launches
         coll = setup_dist(1)
         dev = torch.device("cuda", 0)
@@ -820,7 +895,9 @@ def main():
     cpu = None
     legs = {}
     t0 = time.perf_counter()
-    if single and not args.no_cpu_baseline and args.only is None:
+    if rank0 and not args.no_cpu_baseline and args.only is None:
+        # at N > 1 under torchrun the other ranks wait in the rendezvous meanwhile; the
+        # baseline is the reference's configs[2] job (K gloo node processes) on this host
         cpu = cpu_baseline_diloco(args.model, args.replicas)
     legs["cpu_baseline_s"] = round(time.perf_counter() - t0, 1)
     args.pmc = (None, "not measured (N > 1 or --no-pmc)")

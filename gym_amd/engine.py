@@ -179,8 +179,9 @@ class DiLoCoOuter:
     + broadcast, the outer-optimizer state / world per GPU."""
 
     def __init__(self, coll: Collective, K_local, n, device, dtype, lr=0.7, momentum=0.9, nesterov=True,
-                 dampening=0.0, weight_decay=0.0, shard=None, chunks=None):
+                 dampening=0.0, weight_decay=0.0, shard=None, chunks=None, placement=True):
         self.coll, self.K_local = coll, int(K_local)
+        self.place_opt = placement  # False: never probe / move master+momentum (gym_amd.placement.policy)
         self.K_total = coll.world * self.K_local
         self.hp = dict(lr=lr, momentum=momentum, nesterov=nesterov, dampening=dampening, weight_decay=weight_decay)
         W, X = coll.world, coll.exchange
@@ -245,11 +246,15 @@ class DiLoCoOuter:
             return
         self._placed_for = key
         per = self.per
+        from . import placement
+        ok, why = placement.policy(self.place_opt)
+        if not ok:
+            self.placement = {"placed": False, "why": why}
+            return
         if (self.coll.exchange or reps.device.type != "cuda" or reps.dtype != torch.float32 or self.mom is None
                 or reps.shape[0] > 16 or 4 * per < SHARD_MIN_BYTES or PLACEMENT_CANDIDATES < 2
                 or reps.stride(1) != 1 or reps.stride(0) % 4 or per % 4):
             return
-        from . import placement
         src = reps[:, :per]
 
         def probe_state(state):
@@ -265,7 +270,6 @@ class DiLoCoOuter:
             self._state, self._placed = st, best_buf
             self.master, self.mom = st[:per], st[per:]
         del src
-        torch.cuda.empty_cache()
         self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
                           "how": "master+momentum in fresh device allocations probed with the step's "
                                  "access pattern; candidate 0 = the ordinary allocation"}

@@ -56,7 +56,7 @@ class ArenaAdam(torch.optim.Optimizer):
     each replica clipped by its own gradient norm)."""
 
     def __init__(self, params, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=None, decoupled=True,
-                 **ignored):
+                 placement=True, **ignored):
         if weight_decay is None:
             weight_decay = 1e-2 if decoupled else 0.0  # torch's AdamW / Adam defaults
         if not 0.0 <= lr:
@@ -100,7 +100,8 @@ class ArenaAdam(torch.optim.Optimizer):
         self._partials = ops.sumsq_partials(dev, self.K)
         self._clip = torch.ones(2 * self.K, dtype=torch.float32, device=dev)
         self._placed = None  # the candidate buffer holding M and V once _place chose one
-        self.placement = None
+        self.placement = None  # the placement record (probe times, or why it was skipped)
+        self.place_opt = placement  # False: never probe / move the moments (gym_amd.placement.policy)
 
     def _bind_state(self, p):
         k, o, n = self._where[id(p)]
@@ -146,6 +147,10 @@ class ArenaAdam(torch.optim.Optimizer):
                 or self.ld % 4 or self.P.stride(-1) != 1):
             return
         from . import placement
+        ok, why = placement.policy(self.place_opt)
+        if not ok:
+            self.placement = {"placed": False, "why": why}
+            return
         KL = self.K * self.ld
 
         def probe(M, V):
@@ -167,7 +172,6 @@ class ArenaAdam(torch.optim.Optimizer):
             self.exp_avg, self.exp_avg_sq = self.M.view(-1), self.V.view(-1)
             for p in self.param_groups[0]["params"]:
                 self._bind_state(p)
-            torch.cuda.empty_cache()
         self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": chosen}
 
     def _ranges(self, k):

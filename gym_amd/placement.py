@@ -22,143 +22,54 @@ At GPT-2 124M x 8 the DiLoCo candidates fall in the 1.88 / 1.74 / 1.69 /
 1.76 ms classes and the chosen one runs the bench's step at 1.70 ms (frac
 0.731, profiles/r04w_*).
 
-PlacedBuffer -- one hipMemCreate allocation mapped at its own virtual range,
-wrapped via __cuda_array_interface__ -- is kept for the experiments under
-tools/ only: its candidates reach 1.65-1.66 ms, but on this stack such
-allocations were seen corrupted when interleaved with ordinary ones
-(profiles/r04u_vmm_alias.txt), and the product's bit-exact churn test failed
-with them once inside the full GPU suite.  This module only moves memory;
-every kernel stays behind the C ABI.
+Policy (round 5): placement is on by default and can be turned off per
+strategy / optimizer (`placement=False`, e.g. DiLoCoStrategy(placement=False),
+DeMo(..., placement=False)) or for the process (GA_PLACEMENT=0); it is skipped
+by itself when several processes of the job share one GPU (more ranks than
+visible devices, e.g. nodes over gloo on one card), since each would size its
+candidates from the same free memory.  `policy()` decides and says why; the
+engines record the decision and the probe times in their `placement` record,
+which the strategies expose in __config__().
+
+hipMemCreate candidates (tools/placed_buffer.py) reach the same classes but were
+seen corrupted on this stack when interleaved with ordinary allocations
+(profiles/r04u_vmm_alias.txt); they are kept for experiments under tools/ only.
+This module only moves memory; every kernel stays behind the C ABI.
 """
-import ctypes
 import os
 
 import torch
+import torch.distributed as dist
 
 
-class _Location(ctypes.Structure):
-    _fields_ = [("type", ctypes.c_int), ("id", ctypes.c_int)]
+def device_shared():
+    """True when this process shares its GPU with other ranks of the job (more
+    ranks in the default process group than visible devices: the reference's
+    nodes-over-gloo-on-one-card layout)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", dist.get_world_size()))
+    return local > max(1, torch.cuda.device_count())
 
 
-class _AllocProp(ctypes.Structure):  # hipMemAllocationProp (hip_runtime_api.h)
-    _fields_ = [("type", ctypes.c_int), ("requestedHandleType", ctypes.c_int), ("location", _Location),
-                ("win32HandleMetaData", ctypes.c_void_p), ("compressionType", ctypes.c_ubyte),
-                ("gpuDirectRDMACapable", ctypes.c_ubyte), ("usage", ctypes.c_ushort)]
-
-
-class _AccessDesc(ctypes.Structure):  # hipMemAccessDesc
-    _fields_ = [("location", _Location), ("flags", ctypes.c_int)]
-
-
-_PINNED, _LOC_DEVICE, _PROT_RW, _GRAN_MIN = 1, 1, 3, 0
-_HIP = None
-
-
-def _hip():
-    """The HIP runtime torch itself runs on (already loaded in this process)."""
-    global _HIP
-    if _HIP is None:
-        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
-        lib = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")
-        vp, sz = ctypes.c_void_p, ctypes.c_size_t
-        sig = {"hipMemGetAllocationGranularity": [ctypes.POINTER(sz), ctypes.POINTER(_AllocProp), ctypes.c_int],
-               "hipMemCreate": [ctypes.POINTER(vp), sz, ctypes.POINTER(_AllocProp), ctypes.c_ulonglong],
-               "hipMemAddressReserve": [ctypes.POINTER(vp), sz, sz, vp, ctypes.c_ulonglong],
-               "hipMemMap": [vp, sz, sz, vp, ctypes.c_ulonglong],
-               "hipMemSetAccess": [vp, sz, ctypes.POINTER(_AccessDesc), sz],
-               "hipMemUnmap": [vp, sz], "hipMemRelease": [vp], "hipMemAddressFree": [vp, sz]}
-        for name, args in sig.items():
-            fn = getattr(lib, name)
-            fn.argtypes, fn.restype = args, ctypes.c_int
-        _HIP = lib
-    return _HIP
-
-
-def _check(rc, what):
-    if rc != 0:
-        raise RuntimeError(f"{what} failed (hipError {rc})")
-
-
-def _prop(device_index):
-    p = _AllocProp()
-    p.type, p.requestedHandleType = _PINNED, 0
-    p.location = _Location(_LOC_DEVICE, device_index)
-    return p
-
-
-def granularity(device):
-    g = ctypes.c_size_t(0)
-    p = _prop(torch.device(device).index or 0)
-    _check(_hip().hipMemGetAllocationGranularity(ctypes.byref(g), ctypes.byref(p), _GRAN_MIN),
-           "hipMemGetAllocationGranularity")
-    return max(int(g.value), 1)
-
-
-class _CAI:
-    def __init__(self, ptr, numel, typestr):
-        self.__cuda_array_interface__ = {"shape": (int(numel),), "typestr": typestr, "data": (int(ptr), False),
-                                         "strides": None, "version": 2}
-
-
-class PlacedBuffer:
-    """One physical allocation of `nbytes` (rounded up to whole 2 MiB pages)
-    mapped read-write at a virtual range of its own, on `device`.  Experiments
-    only (tools/): not used by the product, see the module docstring."""
-
-    ALIGN = 2 << 20  # virtual alignment of the mapping
-
-    def __init__(self, nbytes, device):
-        dev = torch.device(device)
-        self.device = dev
-        # whole 2 MiB pages (the minimum granularity the driver reports is 4 KiB);
-        # see profiles/r04u_vmm_alias.txt for what is and is not safe with these
-        # allocations on this stack
-        gran = max(granularity(dev), self.ALIGN)
-        self.nbytes = -(-int(nbytes) // gran) * gran
-        hip = _hip()
-        self.handle, self.va = ctypes.c_void_p(), ctypes.c_void_p()
-        prop = _prop(dev.index or 0)
-        _check(hip.hipMemCreate(ctypes.byref(self.handle), self.nbytes, ctypes.byref(prop), 0), "hipMemCreate")
-        try:
-            _check(hip.hipMemAddressReserve(ctypes.byref(self.va), self.nbytes, self.ALIGN, None, 0),
-                   "hipMemAddressReserve")
-            _check(hip.hipMemMap(self.va, self.nbytes, 0, self.handle, 0), "hipMemMap")
-            acc = _AccessDesc(_Location(_LOC_DEVICE, dev.index or 0), _PROT_RW)
-            _check(hip.hipMemSetAccess(self.va, self.nbytes, ctypes.byref(acc), 1), "hipMemSetAccess")
-        except Exception:
-            self.release()
-            raise
-
-    def tensor(self, dtype=torch.float32):
-        """A 1-D tensor over the whole mapping (borrowed: this object owns the memory)."""
-        esz = torch.empty((), dtype=dtype).element_size()
-        typestr = {torch.float32: "<f4", torch.bfloat16: "<V2", torch.uint8: "|u1"}[dtype]
-        t = torch.as_tensor(_CAI(self.va.value, self.nbytes // esz, typestr), device=self.device)
-        return t if t.dtype == dtype else t.view(dtype)
-
-    def release(self):
-        hip = _hip()
-        if self.va.value:
-            hip.hipMemUnmap(self.va, self.nbytes)
-            hip.hipMemAddressFree(self.va, self.nbytes)
-            self.va = ctypes.c_void_p()
-        if self.handle.value:
-            hip.hipMemRelease(self.handle)
-            self.handle = ctypes.c_void_p()
-
-    def __del__(self):
-        try:
-            torch.cuda.synchronize(self.device)  # no kernel may still use the mapping
-            self.release()
-        except Exception:
-            pass
+def policy(requested=True):
+    """(enabled, reason): whether a step may probe and move its buffers now.
+    requested = the owner's `placement` option (True by default)."""
+    if requested is False:
+        return False, "placement=False"
+    if os.environ.get("GA_PLACEMENT", "1") == "0":
+        return False, "GA_PLACEMENT=0"
+    if device_shared():
+        return False, "GPU shared by several processes of the job"
+    return True, None
 
 
 class DeviceBuffer:
-    """One ordinary device allocation (the caching allocator's, i.e. hipMalloc
-    for a fresh block of this size) with PlacedBuffer's interface: the
-    candidates the product probes.  Held until the choice, so each candidate is
-    distinct memory; `release()` drops it (the caller empties the cache once)."""
+    """One ordinary device allocation: the candidates the product probes.
+    choose() empties the caching allocator's cache first, so each candidate of
+    this size is a new block (its own hipMalloc) rather than cached memory; all
+    are held until the choice, so each is distinct memory; `release()` drops
+    it (choose() empties the cache again afterwards)."""
 
     def __init__(self, nbytes, device):
         self.nbytes = -(-int(nbytes) // 16) * 16
@@ -186,29 +97,35 @@ def time_probe(fn, reps=3):
 
 def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=DeviceBuffer):
     """Create up to max_candidates - 1 allocations of nbytes one at a time (all
-    held until the choice is made, so each is distinct memory; `kind` =
-    DeviceBuffer, ordinary allocations -- what the product uses -- or
-    PlacedBuffer), time probe(buffer) on each, and return (the fastest buffer, or
-    None when none beats baseline_ms -- the caller's own allocation --, every
-    time in creation order with the baseline first).  At most max_frac of the
-    free device memory is taken; running out ends the search with what was
-    probed."""
+    held until the choice is made, so each is distinct memory), time
+    probe(buffer) on each, and return (the fastest buffer, or None when none
+    beats baseline_ms -- the caller's own allocation --, every time in creation
+    order with the baseline first).  At most max_frac of the free device memory
+    is taken; an allocation failure (OutOfMemoryError) ends the search with what
+    was probed.  Any other error -- a rejected or faulting probe launch -- is
+    raised: the search must not hide a poisoned context."""
+    dev = torch.device(device)
+    torch.cuda.empty_cache()  # fresh blocks, not cached free memory
     times = [baseline_ms]
     best, best_t, held = None, baseline_ms, []
-    budget = max_frac * torch.cuda.mem_get_info(torch.device(device))[0]
+    budget = max_frac * torch.cuda.mem_get_info(dev)[0]
     try:
         while len(times) < max_candidates and (len(held) + 1) * nbytes <= budget:
-            buf = kind(nbytes, device)
+            try:
+                buf = kind(nbytes, dev)
+            except torch.cuda.OutOfMemoryError:
+                break
             held.append(buf)
             t = probe(buf)
             times.append(t)
             if t < best_t:
                 best, best_t = buf, t
-    except (RuntimeError, torch.cuda.OutOfMemoryError):
-        pass
-    for b in held:
-        if b is not best:
-            b.release()
+    finally:
+        for b in held:
+            if b is not best:
+                b.release()
+        held = None
+        torch.cuda.empty_cache()
     return best, times
 
 

@@ -116,12 +116,14 @@ class ReplicaRunner:
             spec = s.optim_spec if isinstance(s, SimpleReduceStrategy) else s.inner_optim_spec
             if fusable(spec.cls, spec.kwargs, self.ra):
                 kw = {k: v for k, v in (spec.kwargs or {}).items() if k in ("lr", "betas", "eps", "weight_decay")}
-                self.optim = ArenaAdam(self.ra.params, self.ra, decoupled=spec.cls is torch.optim.AdamW, **kw)
+                self.optim = ArenaAdam(self.ra.params, self.ra, decoupled=spec.cls is torch.optim.AdamW,
+                                       placement=s.placement_opt, **kw)
             else:
                 self.optim = _PerNodeOptim(spec, models, self.ra.arenas)
             if isinstance(s, DiLoCoStrategy):
                 self.max_norm = s.kwargs.get("max_norm")
-                self.outer = DiLoCoOuter(self.coll, self.K, ld, dev, dt, **fused_sgd_hparams(s.outer_optim_spec))
+                self.outer = DiLoCoOuter(self.coll, self.K, ld, dev, dt, placement=s.placement_opt,
+                                         **fused_sgd_hparams(s.outer_optim_spec))
                 self.outer.init_master(self.ra.flat_set[0])
             else:
                 self.max_norm = s.max_norm

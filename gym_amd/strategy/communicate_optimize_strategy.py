@@ -61,5 +61,5 @@ class CommunicateOptimizeStrategy(Strategy):
         self._bind_arena(model)
         for m in self.communication_modules:
             m._init_node(model, rank, num_nodes)
-        self.optim = build_inner_optimizer(self.inner_optim_spec, model, self.arena)
+        self.optim = build_inner_optimizer(self.inner_optim_spec, model, self.arena, self.placement_opt)
         self._setup_scheduler()

@@ -35,7 +35,8 @@ _REQUIRE_GPU = True  # the CPU orchestration tests swap the kernels for oracle s
 class DeMo(torch.optim.SGD):
     def __init__(self, params, compression_decay: float = 0.999, compression_topk: int = 32,
                  compression_chunk: int = 64, weight_decay: float = 0.0,
-                 process_group: Optional[dist.ProcessGroup] = None, custom_all_gather=None, **kwargs):
+                 process_group: Optional[dist.ProcessGroup] = None, custom_all_gather=None, placement: bool = True,
+                 **kwargs):
         super().__init__(params, foreach=False, momentum=0.0, dampening=0.0, nesterov=False, maximize=False,
                          weight_decay=0.0, **kwargs)
         if compression_topk <= 0:
@@ -75,6 +76,9 @@ class DeMo(torch.optim.SGD):
         self.demo_state = {}
         for p, d in zip(trainable, self.arena.layout.views(self.delta_flat)):
             self.demo_state[p] = {"step": 0, "delta": d}
+        # placement=False: the parameters, gradients and deltas stay where they are
+        # (no probe launches, no relocation); see _place
+        self.place_opt = placement
         self.placement, self._placed = None, None
         itemsize = torch.finfo(self.default_dtype).bits // 8
         ref = self.codec.reference_bytes if isinstance(self.codec, PipelinedDeMoCodec) else self.codec.plan.reference_bytes
@@ -84,7 +88,19 @@ class DeMo(torch.optim.SGD):
         """Once, after the first step: move the gradient, parameter and delta
         arenas into the device allocations the step's kernels run fastest on
         (engine.place_demo_step; the probe decodes at lr = 0, encodes into a
-        scratch payload and restores P, G and D, so the results are unchanged)."""
+        scratch payload and restores P, G and D, so the results are unchanged).
+
+        This RE-POINTS every trainable parameter's storage (`p.data`) and its
+        `.grad` at views of the new buffers (the values are identical).  A
+        caller that captured the old storage -- a CUDA/HIP graph of the forward
+        and backward, a tensor alias, an EMA keyed by data_ptr -- must take it
+        again after the first step, or pass placement=False (INTEGRATION.md,
+        caller contract)."""
+        from ...placement import policy
+        ok, why = policy(self.place_opt)
+        if not ok:
+            self.placement = {"placed": False, "why": why}
+            return
         bufs, tens, rec = self.codec.place(P, G, D, lr, self.compression_decay)
         self.placement = rec or {"placed": False}
         if bufs is not None and tens is not None and any(b is not None for b in bufs):

@@ -61,14 +61,15 @@ class DiLoCoStrategy(Strategy):
         hp = fused_sgd_hparams(self.outer_optim_spec)
         self.outer_optimizer = None
         if hp is not None:
-            self.engine = DiLoCoOuter(self.coll, 1, arena.n, arena.device, arena.dtype, **hp)
+            self.engine = DiLoCoOuter(self.coll, 1, arena.n, arena.device, arena.dtype, placement=self.placement_opt,
+                                      **hp)
             self.engine.init_master(arena.flat)
         else:
             self.engine = None
             self.master = torch.nn.Parameter(arena.flat.detach().float().clone())
             self.outer_optimizer = self.outer_optim_spec.build([self.master])
             self._avg = torch.empty_like(arena.flat)
-        self.optim = build_inner_optimizer(self.inner_optim_spec, model, arena)
+        self.optim = build_inner_optimizer(self.inner_optim_spec, model, arena, self.placement_opt)
         self._setup_scheduler()
 
     def _outer_step(self):

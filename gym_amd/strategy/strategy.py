@@ -36,7 +36,7 @@ def require_gpu(device):
                            "Move it to a cuda device (one process per GPU).")
 
 
-def build_inner_optimizer(spec, model, arena):
+def build_inner_optimizer(spec, model, arena, placement=True):
     """The node's inner optimizer: torch's AdamW/Adam become ArenaAdam (one fused
     kernel over the arena per step, gym_amd.fused_optim); any other OptimSpec is
     built as in the reference (OptimSpec.build, optim.py:38-39).  GA_FUSED_OPTIM=0
@@ -45,7 +45,7 @@ def build_inner_optimizer(spec, model, arena):
     from ..fused_optim import ArenaAdam, fusable
     if os.environ.get("GA_FUSED_OPTIM", "1") != "0" and fusable(spec.cls, spec.kwargs, arena):
         kw = {k: v for k, v in (spec.kwargs or {}).items() if k in ("lr", "betas", "eps", "weight_decay")}
-        return ArenaAdam(model.parameters(), arena, decoupled=spec.cls is torch.optim.AdamW, **kw)
+        return ArenaAdam(model.parameters(), arena, decoupled=spec.cls is torch.optim.AdamW, placement=placement, **kw)
     return spec.build(model)
 
 
@@ -145,10 +145,29 @@ class Strategy(ABC, LogModule):
         else:
             self.scheduler = None
 
+    @property
+    def placement_opt(self):
+        """The `placement` kwarg (default True): False keeps every buffer of the
+        step where it was allocated -- no probe launches, no relocation
+        (gym_amd.placement.policy)."""
+        return self.kwargs.get("placement", True)
+
+    def placement_records(self):
+        """What each placement-capable part of this node's step decided: probe
+        times and the chosen candidate, or why it was skipped (None: not yet
+        run or not applicable)."""
+        out = {}
+        for name in ("engine", "optim"):
+            rec = getattr(getattr(self, name, None), "placement", None)
+            if rec is not None and not isinstance(rec, bool):
+                out[name] = rec
+        return out
+
     def __config__(self):
         cfg = super().__config__(["iteration", "local_step", "lr_callbacks", "model", "optim", "scheduler",
                                   "arena", "coll", "engine"])
         cfg["strategy"] = self.__class__.__name__
+        cfg["placement"] = {"enabled": self.placement_opt is not False, "records": self.placement_records()}
         return cfg
 
 
@@ -165,7 +184,7 @@ class SimpleReduceStrategy(Strategy):
         super()._init_node(model, rank, num_nodes)
         arena = self._bind_arena(model)
         self.engine = MeanReduce(self.coll, 1, arena.n, arena.device, arena.dtype)
-        self.optim = build_inner_optimizer(self.optim_spec, model, arena)
+        self.optim = build_inner_optimizer(self.optim_spec, model, arena, self.placement_opt)
         self._setup_scheduler()
 
     def step(self):

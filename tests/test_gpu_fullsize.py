@@ -498,3 +498,58 @@ def test_pipelined_demo_codec_placement_restores_and_matches():
     codec(Pm, Gm, Dm, 1e-3)
     for a, b in zip((P1, G1, D1), (Pm, Gm, Dm)):
         assert torch.equal(a, b)
+
+
+def test_placement_false_bit_identical_without_probe_launches(monkeypatch):
+    """placement=False on the DiLoCo engine, the fused AdamW and the DeMo
+    optimizer: no probe kernel is launched and no candidate is allocated (the
+    probes and the candidate search raise if called), the records say why, and
+    the steps are bit-identical to the placed run."""
+    from gym_amd import ops, placement
+    from gym_amd import engine as E
+    from gym_amd.arena import ReplicaArena
+    from gym_amd.comm import Collective
+    from gym_amd.fused_optim import ArenaAdam
+    from gym_amd.strategy.demo_impl.demo import DeMo
+    torch.manual_seed(0)
+    base = torch.nn.Sequential(*[torch.nn.Linear(2048, 2048) for _ in range(3)]).to(DEV)  # 12.6M params
+    x = torch.randn(64, 2048, device=DEV)
+
+    def run(placed):
+        ra = ReplicaArena([copy.deepcopy(base) for _ in range(4)])
+        opt = ArenaAdam(ra.params, ra, lr=1e-3, weight_decay=0.01, placement=placed)
+        eng = E.DiLoCoOuter(Collective(), 4, ra.ld, DEV, torch.float32, placement=placed)
+        eng.init_master(ra.flat_set[0])
+        g = torch.Generator(device=DEV)
+        g.manual_seed(5)
+        for _ in range(2):
+            for _ in range(2):
+                for p in ra.params:
+                    p.grad = torch.randn(p.shape, device=DEV, generator=g) * 1e-2
+                opt.step()
+            eng(ra.flat_set)
+        model = copy.deepcopy(base)
+        dm = DeMo(model.parameters(), lr=1e-3, compression_topk=32, compression_chunk=64, placement=placed)
+        for s in range(2):
+            dm.zero_grad()
+            model(x).square().mean().backward()
+            for p in model.parameters():
+                p.grad.copy_(torch.randn(p.shape, device=DEV, generator=g) * 1e-2)
+            dm.step()
+        out = [t.clone() for t in (ra.flat_set, eng.master, eng.mom, opt.M, opt.V)]
+        out += [p.detach().clone() for p in model.parameters()]
+        return out, (opt.placement, eng.placement, dm.placement)
+
+    placed, recs_on = run(True)
+    assert recs_on[1] is not None and recs_on[1].get("candidates", 0) >= 2
+
+    def boom(*a, **k):
+        raise AssertionError("placement probe launched with placement=False")
+    for name in ("probe_diloco_placement", "probe_adam_placement"):
+        monkeypatch.setattr(ops, name, boom)
+    monkeypatch.setattr(placement, "choose", boom)
+    monkeypatch.setattr(placement, "place_each", boom)
+    plain, recs_off = run(False)
+    assert all(r == {"placed": False, "why": "placement=False"} for r in recs_off), recs_off
+    for a, b in zip(placed, plain):
+        assert torch.equal(a, b)

@@ -8,7 +8,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from gym_amd.placement import PlacedBuffer  # noqa: E402
+from placed_buffer import PlacedBuffer  # noqa: E402
 
 DEV = torch.device("cuda:0")
 

@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gym_amd import ops  # noqa: E402
 from gym_amd.arena import ArenaLayout  # noqa: E402
-from gym_amd.placement import PlacedBuffer  # noqa: E402
+from placed_buffer import PlacedBuffer  # noqa: E402
 from gym_amd.shapes import MODELS  # noqa: E402
 
 
