@@ -547,14 +547,31 @@ def bench_sparta_replica_step(args, coll, dev, K=32, p=0.005, model="gpt2-124m")
     hp = dict(lerp_w=0.1, beta2=0.999, one_m_beta2=1 - 0.999, eps=1e-8, wd_factor=1 - 1e-3 * 0.01, l2_wd=0.0,
               step_size=-1e-3 / 0.1, bc2_sqrt=(1 - 0.999) ** 0.5)
     reps = max(5, args.steps // 2)
-    adam = queued_ms(lambda: ops.adam_step(P, G, M, V, **hp), reps, dev)
-    step = queued_ms(lambda: (ops.adam_step(P, G, M, V, **hp),
+    adam_one = queued_ms(lambda: ops.adam_step(P, G, M, V, **hp), reps, dev)  # one launch, ordinary moments
+    # the product's step (fused_optim.ArenaAdam at K > 1): each replica's moment rows placed
+    # on their own against that replica's parameter / gradient rows, one launch per replica
+    from gym_amd.fused_optim import place_moment_rows
+    Mr, Vr, bufs, prec = place_moment_rows(P, G, list(M.unbind(0)), list(V.unbind(0)))
+    if any(b is not None for b in bufs):
+        del M, V
+        torch.cuda.empty_cache()
+
+    def adam_rows():
+        for k in range(K):
+            ops.adam_step(P[k], G[k], Mr[k], Vr[k], **hp)
+    adam = queued_ms(adam_rows, reps, dev)
+    step = queued_ms(lambda: (adam_rows(),
                               ops.sparta_average_local(P, ld, float(K), mask=draw, layout="rows")), reps, dev)
     alg = 28 * K * ld  # read p, g, m, v; write p, m, v
-    del P, G, M, V
+    del P, G, Mr, Vr, bufs
     return {"model": model, "K": K, "p": p, "mask": "the reference's torch.bernoulli draw, in-kernel",
             "adamw_alone_ms": round(adam, 4), "adamw_then_sparta_ms": round(step, 4),
             "added_ms": round(step - adam, 4),
+            "adamw_what": "ArenaAdam's K > 1 step: moment rows placed per replica (place_moment_rows), one "
+                          "ga_adam_step launch per replica",
+            "adamw_one_launch_unplaced_ms": round(adam_one, 4),
+            "adamw_one_launch_unplaced_frac_hbm": round(alg / (adam_one * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "placement": {k: v for k, v in prec.items() if k != "probe_ms"},
             "adamw_alg_GBps": round(alg / (adam * 1e-3) / 1e9, 1),
             "adamw_frac_hbm": round(alg / (adam * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 

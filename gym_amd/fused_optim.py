@@ -29,6 +29,9 @@ _UNSUPPORTED = ("amsgrad", "maximize", "capturable", "differentiable")
 PLACEMENT_CANDIDATES = 48
 PLACEMENT_MAX_FRAC = 0.3
 PLACEMENT_MIN_BYTES = 32 << 20
+# K > 1 replicas: each replica's moments are placed on their own (probed against that
+# replica's parameter / gradient rows), with fewer candidates per replica
+PLACEMENT_ROW_CANDIDATES = 16
 
 
 def fusable(spec_cls, kwargs, arena):
@@ -48,6 +51,52 @@ def fusable(spec_cls, kwargs, arena):
         return False
     lr = kw.get("lr", 1e-3)
     return not isinstance(lr, torch.Tensor)
+
+
+def place_moment_rows(P, G, Mr, Vr, max_candidates=None, max_frac=None):
+    """Per-replica placement of Adam moments (ArenaAdam, K > 1): for each
+    replica k, up to max_candidates fresh allocations of its two moment rows
+    are timed with ga_probe_adam_placement against P[k], G[k] (values
+    unchanged) beside Mr[k], Vr[k] where they are; the fastest keeps them.
+    Returns (new rows M, new rows V -- candidate views or copies of the old
+    rows --, per replica the chosen buffer or None, the record)."""
+    from . import placement
+    max_candidates = PLACEMENT_ROW_CANDIDATES if max_candidates is None else max_candidates
+    max_frac = PLACEMENT_MAX_FRAC if max_frac is None else max_frac
+    K, ld = P.shape[0], Mr[0].numel()
+    bufs, probe_ms, chosen = [], [], []
+    for k in range(K):
+        Pk, Gk = P[k, :ld], G[k, :ld]
+
+        def probe(M, V):
+            return placement.time_probe(lambda: ops.probe_adam_placement(Pk, Gk, M, V))
+
+        def split(buf):
+            t = buf.tensor()
+            return t[:ld], t[ld:2 * ld]
+
+        best, times = placement.choose(2 * ld * 4, P.device, lambda b: probe(*split(b)), probe(Mr[k], Vr[k]),
+                                       max_candidates, max_frac)
+        bufs.append(best)
+        probe_ms.append([round(t, 4) for t in times])
+        chosen.append(min(range(len(times)), key=lambda i: times[i]) if best is not None else 0)
+    outM, outV = [], []
+    any_placed = any(b is not None for b in bufs)
+    for k, b in enumerate(bufs):
+        if b is None:  # kept where they are (copies when the [K, ld] pair is released)
+            m, v = (Mr[k].clone(), Vr[k].clone()) if any_placed else (Mr[k], Vr[k])
+        else:
+            t = b.tensor()
+            m, v = t[:ld], t[ld:2 * ld]
+            m.copy_(Mr[k])
+            v.copy_(Vr[k])
+        outM.append(m)
+        outV.append(v)
+    rec = {"per_replica": True, "candidates_per_replica": max_candidates, "chosen": chosen,
+           "placed_rows": sum(b is not None for b in bufs),
+           "probe_ms_ordinary_sum": round(sum(t[0] for t in probe_ms), 4),
+           "probe_ms_chosen_sum": round(sum(min(t) for t in probe_ms), 4), "probe_ms": probe_ms}
+    return outM, outV, bufs, rec
 
 
 class ArenaAdam(torch.optim.Optimizer):
@@ -79,9 +128,12 @@ class ArenaAdam(torch.optim.Optimizer):
         self.G = arena.grad_set if hasattr(arena, "grad_set") else arena.grad_flat.view(1, -1)
         self.K, self.ld = self.P.shape
         dev = self.P.device
-        self.M = torch.zeros_like(self.P, dtype=torch.float32)
-        self.V = torch.zeros_like(self.P, dtype=torch.float32)
-        self.exp_avg, self.exp_avg_sq = self.M.view(-1), self.V.view(-1)  # flat views (single-arena users)
+        self._M = torch.zeros_like(self.P, dtype=torch.float32)
+        self._V = torch.zeros_like(self.P, dtype=torch.float32)
+        # per replica [ld] rows of the moments: views of _M / _V, or (after a per-replica
+        # placement) each in its own candidate buffer, when _M / _V are None
+        self._Mr, self._Vr = list(self._M.unbind(0)), list(self._V.unbind(0))
+        self.exp_avg, self.exp_avg_sq = self._M.view(-1), self._V.view(-1)  # flat views (single-arena users)
         self._step_t = torch.tensor(0.0)
         where = {}
         for k, ar in enumerate(self.arenas):
@@ -103,10 +155,19 @@ class ArenaAdam(torch.optim.Optimizer):
         self.placement = None  # the placement record (probe times, or why it was skipped)
         self.place_opt = placement  # False: never probe / move the moments (gym_amd.placement.policy)
 
+    @property
+    def M(self):
+        """exp_avg as [K, ld] (a stacked copy once the rows were placed apart)."""
+        return self._M if self._M is not None else torch.stack(self._Mr)
+
+    @property
+    def V(self):
+        return self._V if self._V is not None else torch.stack(self._Vr)
+
     def _bind_state(self, p):
         k, o, n = self._where[id(p)]
-        self.state[p] = {"step": self._step_t, "exp_avg": self.M[k, o:o + n].view(p.shape),
-                         "exp_avg_sq": self.V[k, o:o + n].view(p.shape)}
+        self.state[p] = {"step": self._step_t, "exp_avg": self._Mr[k][o:o + n].view(p.shape),
+                         "exp_avg_sq": self._Vr[k][o:o + n].view(p.shape)}
 
     def load_state_dict(self, state_dict):
         """torch's Optimizer.load_state_dict, then the loaded per-parameter
@@ -116,14 +177,14 @@ class ArenaAdam(torch.optim.Optimizer):
         super().load_state_dict(state_dict)
         steps = set()
         with torch.no_grad():
-            self.M.zero_()
-            self.V.zero_()
+            for r in self._Mr + self._Vr:
+                r.zero_()
             for p in self.param_groups[0]["params"]:
                 st = self.state.get(p, {})
                 k, o, n = self._where[id(p)]
                 if "exp_avg" in st:
-                    self.M[k, o:o + n].copy_(st["exp_avg"].reshape(-1))
-                    self.V[k, o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                    self._Mr[k][o:o + n].copy_(st["exp_avg"].reshape(-1))
+                    self._Vr[k][o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
                 if "step" in st:
                     steps.add(float(st["step"]))
         if len(steps) > 1:
@@ -137,12 +198,19 @@ class ArenaAdam(torch.optim.Optimizer):
         """Choose the physical memory of the moments, once, before the first
         step: the fused step's rate depends on where exp_avg / exp_avg_sq sit
         physically relative to the parameters and gradients (0.553-0.625 ms at
-        GPT-2 124M, profiles/r04k_adam_placement.txt; gym_amd.placement), so up
-        to PLACEMENT_CANDIDATES fresh device allocations are timed with
-        ga_probe_adam_placement (the step's access pattern, values unchanged)
-        beside the ordinary ones and the fastest keeps the moments."""
+        GPT-2 124M, profiles/r04k_adam_placement.txt; gym_amd.placement), so
+        fresh device allocations are timed with ga_probe_adam_placement (the
+        step's access pattern, values unchanged) beside the ordinary ones and
+        the fastest keeps the moments.  One replica (K = 1): up to
+        PLACEMENT_CANDIDATES buffers for both moments.  K > 1: replica by
+        replica, up to PLACEMENT_ROW_CANDIDATES buffers of one replica's two
+        moment rows each, probed against that replica's parameter / gradient
+        rows (the kernel's replica-major grid streams one replica's four rows
+        at a time; a [K, ld] candidate at K = 32 x 124M would be 32 GB, so the
+        memory budget would leave no choice); the step then runs one launch
+        per replica."""
         self._place_done = True
-        nb = 2 * self.M.numel() * 4
+        nb = 2 * self.K * self.ld * 4
         if (self.P.device.type != "cuda" or nb < PLACEMENT_MIN_BYTES or PLACEMENT_CANDIDATES < 2
                 or self.ld % 4 or self.P.stride(-1) != 1):
             return
@@ -151,6 +219,12 @@ class ArenaAdam(torch.optim.Optimizer):
         if not ok:
             self.placement = {"placed": False, "why": why}
             return
+        if self.K == 1:
+            self._place_whole(placement, nb)
+        else:
+            self._place_rows(placement)
+
+    def _place_whole(self, placement, nb):
         KL = self.K * self.ld
 
         def probe(M, V):
@@ -160,19 +234,31 @@ class ArenaAdam(torch.optim.Optimizer):
             t = buf.tensor()
             return t[:KL].view(self.K, self.ld), t[KL:2 * KL].view(self.K, self.ld)
 
-        best, times = placement.choose(nb, self.P.device, lambda b: probe(*split(b)), probe(self.M, self.V),
+        best, times = placement.choose(nb, self.P.device, lambda b: probe(*split(b)), probe(self._M, self._V),
                                        PLACEMENT_CANDIDATES, PLACEMENT_MAX_FRAC)
         chosen = 0
         if best is not None:
             chosen = min(range(len(times)), key=lambda i: times[i])
             M, V = split(best)
-            M.copy_(self.M)
-            V.copy_(self.V)
-            self.M, self.V, self._placed = M, V, best
-            self.exp_avg, self.exp_avg_sq = self.M.view(-1), self.V.view(-1)
+            M.copy_(self._M)
+            V.copy_(self._V)
+            self._M, self._V, self._placed = M, V, best
+            self._Mr, self._Vr = list(M.unbind(0)), list(V.unbind(0))
+            self.exp_avg, self.exp_avg_sq = M.view(-1), V.view(-1)
             for p in self.param_groups[0]["params"]:
                 self._bind_state(p)
         self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": chosen}
+
+    def _place_rows(self, placement):
+        Mr, Vr, bufs, rec = place_moment_rows(self.P, self.G, self._Mr, self._Vr)
+        if any(b is not None for b in bufs):
+            self._Mr, self._Vr, self._placed = Mr, Vr, bufs
+            self._M = self._V = None
+            self.exp_avg = self.exp_avg_sq = None
+            for p in self.param_groups[0]["params"]:
+                self._bind_state(p)
+            torch.cuda.empty_cache()
+        self.placement = rec
 
     def _ranges(self, k):
         """Contiguous ranges [a, b) of replica k's arena whose parameters have a
@@ -213,11 +299,11 @@ class ArenaAdam(torch.optim.Optimizer):
         if max_norm:
             ops.grad_clip_coef(self.G, self.ld, max_norm, self._partials, self._clip)
             clip = self._clip
-        if all(r == [(0, self.ld)] for r in ranges):
-            ops.adam_step(self.P, self.G, self.M, self.V, clip_coef=clip, **hp)
+        if self._M is not None and all(r == [(0, self.ld)] for r in ranges):
+            ops.adam_step(self.P, self.G, self._M, self._V, clip_coef=clip, **hp)
             return loss
-        for k in range(self.K):
+        for k in range(self.K):  # per replica (its moments placed apart, or partial ranges)
             ck = clip[2 * k:2 * k + 2] if clip is not None else None
             for a, b in ranges[k]:
-                ops.adam_step(self.P[k, a:b], self.G[k, a:b], self.M[k, a:b], self.V[k, a:b], clip_coef=ck, **hp)
+                ops.adam_step(self.P[k, a:b], self.G[k, a:b], self._Mr[k][a:b], self._Vr[k][a:b], clip_coef=ck, **hp)
         return loss

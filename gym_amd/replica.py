@@ -13,7 +13,8 @@ its own data shard (DistributedSampler(num_replicas=num_nodes, rank=node) or
 the dataset factory called with the node's rank), gradient accumulation over
 batch_size // minibatch_size minibatches with `grad /= batch_size /
 minibatch_size`, its own clip_grad_norm_, then the strategy step.  Supported
-strategies: SimpleReduce, DiLoCo (SGD-family outer optimizer), SPARTA (every
+strategies: SimpleReduce, DiLoCo (any outer optimizer: the fused kernel for
+SGD-family, torch's optimizer on an fp32 master otherwise), SPARTA (every
 selector: the torch-drawn masks of node 0 -- the reference uses rank 0's --
 or the Philox stream), FedAvg (full or island averaging), DeMo.  Anything else runs on
 the process-per-node path (ReplicaRunner.supports).
@@ -76,7 +77,7 @@ class ReplicaRunner:
         if isinstance(strategy, FedAvgStrategy):
             return True
         if isinstance(strategy, DiLoCoStrategy):
-            return fused_sgd_hparams(strategy.outer_optim_spec) is not None
+            return True  # any outer OptimSpec: fused kernel for SGD, torch's optimizer on a master otherwise
         return isinstance(strategy, (SimpleReduceStrategy, DeMoStrategy))
 
     def __init__(self, strategy, models, rank, num_nodes):
@@ -122,9 +123,17 @@ class ReplicaRunner:
                 self.optim = _PerNodeOptim(spec, models, self.ra.arenas)
             if isinstance(s, DiLoCoStrategy):
                 self.max_norm = s.kwargs.get("max_norm")
-                self.outer = DiLoCoOuter(self.coll, self.K, ld, dev, dt, placement=s.placement_opt,
-                                         **fused_sgd_hparams(s.outer_optim_spec))
-                self.outer.init_master(self.ra.flat_set[0])
+                hp = fused_sgd_hparams(s.outer_optim_spec)
+                if hp is not None:
+                    self.outer = DiLoCoOuter(self.coll, self.K, ld, dev, dt, placement=s.placement_opt, **hp)
+                    self.outer.init_master(self.ra.flat_set[0])
+                else:
+                    # any other outer OptimSpec (diloco.py:26-28): torch's optimizer on an fp32
+                    # master of node 0's start (diloco.py:81-89), fed the node average
+                    self.outer = self._generic_outer
+                    self.master = torch.nn.Parameter(self.ra.flat_set[0].detach().float().clone())
+                    self.outer_optimizer = s.outer_optim_spec.build([self.master])
+                    self._avg = torch.empty(ld, device=dev, dtype=dt)
             else:
                 self.max_norm = s.max_norm
             self.islands = (isinstance(s, FedAvgStrategy) and s.island_size is not None
@@ -199,6 +208,21 @@ class ReplicaRunner:
             for cb in s.lr_callbacks:
                 cb(self.lr_scheds[0].get_last_lr()[0])
         s.local_step += 1
+
+    def _generic_outer(self, P):
+        """DiLoCo's outer step for a non-SGD outer optimizer (diloco.py:34-49,
+        66-74) over the K local nodes: the ascending fp32 sum of the rows
+        (ga_replica_mean), an all-reduce across processes, true division by
+        num_nodes (the reference's `/= num_nodes`), master.grad = master - avg,
+        the torch optimizer's step, and the master written to every row -- the
+        arithmetic of DiLoCoStrategy._outer_step on each process-per-node rank."""
+        ops.replica_mean(P, self._avg, divisor=1.0)
+        self.coll.all_reduce_(self._avg)
+        ops.replica_mean(self._avg, self._avg, divisor=float(self.num_nodes))
+        self.outer_optimizer.zero_grad()
+        self.master.grad = self.master.detach() - self._avg.float()
+        self.outer_optimizer.step()
+        P.copy_(self.master.detach().to(P.dtype).unsqueeze(0).expand_as(P))
 
     def _island_average(self, P):
         """FedAvg islands (federated_averaging.py:26-69) over the nodes of this

@@ -40,6 +40,9 @@ def make_strategy(name):
         return SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-2), max_norm=1.0)
     if name == "diloco":
         return DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-2), H=2)
+    if name == "diloco_adam":  # a non-SGD outer optimizer (diloco.py:26-28): torch's Adam on the master
+        return DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-2),
+                              outer_optim_spec=OptimSpec(torch.optim.Adam, lr=0.05), H=2)
     if name == "sparta":  # the reference's torch-drawn masks (default)
         return SPARTAStrategy(inner_optim=OptimSpec(torch.optim.AdamW, lr=1e-2), p_sparta=0.1)
     if name == "sparta_philox":

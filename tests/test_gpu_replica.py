@@ -9,7 +9,7 @@ import replica_scenarios as R
 
 pytestmark = pytest.mark.gpu
 
-NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "fedavg_islands", "demo", "demo_frozen",
+NAMES = ["simple", "diloco", "diloco_adam", "sparta", "sparta_philox", "fedavg", "fedavg_islands", "demo", "demo_frozen",
          "sparta_frozen"]
 
 
@@ -26,6 +26,19 @@ def test_replicas_match_process_per_node_gpu(tmp_path, name):
         R.compare(proc, rep, rtol=0, atol=0)
         return
     R.compare(proc, rep)
+
+
+def test_diloco_outer_adam_replicas_bit_exact_gpu(tmp_path):
+    """DiLoCo with a non-SGD outer optimizer (torch Adam) in replica mode: two
+    nodes in one process end bit-identical to two processes over gloo (a sum of
+    two is order-free; the same inner kernel, division and torch Adam)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from gym_amd.replica import ReplicaRunner
+    assert ReplicaRunner.supports(R.make_strategy("diloco_adam"))
+    proc = R.run_process_mode("diloco_adam", 2, "cuda:0", False, str(tmp_path))
+    rep = R.run_replica_mode("diloco_adam", 2, "cuda:0", False)
+    R.compare(proc, rep, rtol=0, atol=0)
 
 
 def test_local_trainer_fit_replica_mode():

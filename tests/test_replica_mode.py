@@ -7,7 +7,7 @@ import pytest
 
 import replica_scenarios as R
 
-NAMES = ["simple", "diloco", "sparta", "sparta_philox", "fedavg", "fedavg_islands", "demo", "demo_frozen",
+NAMES = ["simple", "diloco", "diloco_adam", "sparta", "sparta_philox", "fedavg", "fedavg_islands", "demo", "demo_frozen",
          "sparta_frozen"]
 
 
@@ -44,6 +44,16 @@ def test_replica_processes_match_process_per_node(tmp_path, name):
     proc = R.run_process_mode(name, 4, "cpu", True, str(tmp_path / "p"))
     rep = R.run_replica_processes(name, 2, 2, "cpu", True, str(tmp_path / "r"))
     R.compare(proc, rep)
+
+
+def test_diloco_outer_adam_replicas_bit_exact(tmp_path, fake):
+    """A non-SGD outer optimizer runs in replica mode (ReplicaRunner.supports);
+    two nodes: bit-identical to two processes (a sum of two is order-free)."""
+    from gym_amd.replica import ReplicaRunner
+    assert ReplicaRunner.supports(R.make_strategy("diloco_adam"))
+    proc = R.run_process_mode("diloco_adam", 2, "cpu", True, str(tmp_path))
+    rep = R.run_replica_mode("diloco_adam", 2, "cpu", True)
+    R.compare(proc, rep, rtol=0, atol=0)
 
 
 def test_replica_layout_rules():

@@ -24,7 +24,7 @@ python tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write diloco_outer $O/pmc_traffi
 # exchange forced (rehearsal), and 2 ranks over gloo sharing the GPU (REHEARSE=0 skips both)
 if [ "${REHEARSE:-1}" != "0" ]; then
   GA_BENCH_FORCE_EXCHANGE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29613 bench.py --steps 10 --warmup 2 > $O/bench_rccl1_rehearsal.json 2> $O/bench_rccl1_rehearsal.err || { echo "RCCL1 REHEARSAL FAILED"; tail -20 $O/bench_rccl1_rehearsal.err; exit 1; }
-  GA_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29614 bench.py --gpus 2 --steps 5 --warmup 1 > $O/bench_gloo2_rehearsal.json 2> $O/bench_gloo2_rehearsal.err || { echo "GLOO2 REHEARSAL FAILED"; tail -20 $O/bench_gloo2_rehearsal.err; exit 1; }
+  GA_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 1 > $O/bench_gloo2_rehearsal.json 2> $O/bench_gloo2_rehearsal.err || { echo "GLOO2 REHEARSAL FAILED"; tail -20 $O/bench_gloo2_rehearsal.err; exit 1; }
   tail -c 400 $O/bench_gloo2_rehearsal.json
 fi
 echo DONE
