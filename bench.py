@@ -525,15 +525,13 @@ def bench_sparta(args, coll, dev, K_total=32, p=0.005, model="gpt2-124m", layout
 
 def bench_sparta_replica_step(args, coll, dev, K=32, p=0.005, model="gpt2-124m"):
     """configs[3] as the replica training loop runs it (gym_amd.replica, one GPU):
-    the inner AdamW over the 32 nodes' [K, ld] rows and SPARTA's sparse average
-    with the reference's torch.bernoulli draw (communicate_optimize_strategy.py:
-    67-85, sparta.py:24-44).  The product's step: the draw into packed words,
-    the mask indexed per 4096-element chunk, the AdamW pass writing every
-    selected element's updated value per replica (ga_adam_step_select, one
-    launch per replica over its placed moments), one kernel averaging those
-    into every row -- no read pass over the rows.  added_ms = what SPARTA adds
-    to the AdamW pass; two_launch_* = the round-4 step (AdamW, then
-    ga_sparta_average_local reading every selected word back)."""
+    the inner AdamW over the 32 nodes' [K, ld] rows (ga_adam_step) followed by
+    SPARTA's sparse average with the reference's torch.bernoulli draw in-kernel
+    (ga_sparta_average_local, rows layout; communicate_optimize_strategy.py:67-85).
+    added_ms = what the SPARTA average adds to the AdamW pass.  (A fused
+    element-major AdamW + average pass measured no faster: the element-major
+    traversal of 32 rows costs ~0.9 ms over the replica-major AdamW,
+    profiles/r04f_ubench_adam_sparta.txt.)"""
     if coll.world > 1:
         return {"skipped": "single-GPU replica loop (no exchange)"}
     shapes = MODELS[model]()
@@ -544,7 +542,7 @@ def bench_sparta_replica_step(args, coll, dev, K=32, p=0.005, model="gpt2-124m")
     P = torch.randn(K, ld, device=dev, generator=g).mul_(0.02)
     G = torch.randn(K, ld, device=dev, generator=g).mul_(1e-3)
     M, V = torch.zeros_like(P), torch.zeros_like(P)
-    table, nb = ops.sparta_bernoulli_table(layout.offsets, layout.numels, dev)
+    table, _ = ops.sparta_bernoulli_table(layout.offsets, layout.numels, dev)
     draw = ops.TorchDraw(table, p, 42, 0, 12)
     hp = dict(lerp_w=0.1, beta2=0.999, one_m_beta2=1 - 0.999, eps=1e-8, wd_factor=1 - 1e-3 * 0.01, l2_wd=0.0,
               step_size=-1e-3 / 0.1, bc2_sqrt=(1 - 0.999) ** 0.5)
@@ -558,45 +556,17 @@ def bench_sparta_replica_step(args, coll, dev, K=32, p=0.005, model="gpt2-124m")
         del M, V
         torch.cuda.empty_cache()
 
-    def adam_rows(select=None):
+    def adam_rows():
         for k in range(K):
-            ops.adam_step(P[k], G[k], Mr[k], Vr[k], select=select.row(k) if select is not None else None, **hp)
+            ops.adam_step(P[k], G[k], Mr[k], Vr[k], **hp)
     adam = queued_ms(adam_rows, reps, dev)
-    two = queued_ms(lambda: (adam_rows(),
-                             ops.sparta_average_local(P, ld, float(K), mask=draw, layout="rows")), reps, dev)
-    # the product's step (ReplicaRunner: Sparta.rows_begin / rows_finish): the reference
-    # draw into packed words, the mask indexed per 4096-element chunk, the AdamW pass
-    # writing the selected values, one kernel averaging them into every row
-    from gym_amd.engine import sparta_capacity
-    cap = sparta_capacity(ld, p)
-    bits = torch.zeros(ops.sparta_mask_words(ld), dtype=torch.int64, device=dev)
-    cb = torch.empty(ops.sparta_chunk_count(ld), dtype=torch.int32, device=dev)
-    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
-    sel = ops.RowsSelect(bits, cb, torch.empty(K, cap, device=dev), cap)
-
-    def fused():
-        ops.sparta_torch_bernoulli(table, nb, p, 42, 0, 12, bits)
-        ops.sparta_mask_chunks(bits, ld, cb, cap, cnt)
-        adam_rows(sel)
-        ops.sparta_rows_mean_scatter(P, ld, sel, float(K))
-    step = queued_ms(fused, reps, dev)
-    draw_ms = queued_ms(lambda: ops.sparta_torch_bernoulli(table, nb, p, 42, 0, 12, bits), reps, dev)
-    index_ms = queued_ms(lambda: ops.sparta_mask_chunks(bits, ld, cb, cap, cnt), reps, dev)
-    adam_sel = queued_ms(lambda: adam_rows(sel), reps, dev)
-    mean_ms = queued_ms(lambda: ops.sparta_rows_mean_scatter(P, ld, sel, float(K)), reps, dev)
-    M_sel = int(cnt[0].item())
+    step = queued_ms(lambda: (adam_rows(),
+                              ops.sparta_average_local(P, ld, float(K), mask=draw, layout="rows")), reps, dev)
     alg = 28 * K * ld  # read p, g, m, v; write p, m, v
     del P, G, Mr, Vr, bufs
-    return {"model": model, "K": K, "p": p, "mask": "the reference's torch.bernoulli draw (packed words)",
+    return {"model": model, "K": K, "p": p, "mask": "the reference's torch.bernoulli draw, in-kernel",
             "adamw_alone_ms": round(adam, 4), "adamw_then_sparta_ms": round(step, 4),
             "added_ms": round(step - adam, 4),
-            "path": "ga_sparta_torch_bernoulli -> ga_sparta_mask_chunks -> ga_adam_step_select (per replica) -> "
-                    "ga_sparta_rows_mean_scatter (the replica loop's step, gym_amd.replica)",
-            "parts_ms": {"draw": round(draw_ms, 4), "index": round(index_ms, 4),
-                         "adamw_select_minus_adamw": round(adam_sel - adam, 4), "mean_scatter": round(mean_ms, 4)},
-            "selected": M_sel,
-            "mean_scatter_random_word_writes": K * M_sel,
-            "two_launch_step_ms": round(two, 4), "two_launch_added_ms": round(two - adam, 4),
             "adamw_what": "ArenaAdam's K > 1 step: moment rows placed per replica (place_moment_rows), one "
                           "ga_adam_step launch per replica",
             "adamw_one_launch_unplaced_ms": round(adam_one, 4),

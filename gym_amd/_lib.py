@@ -75,10 +75,6 @@ SIGNATURES = {
     "ga_sparta_scatter": (c_i32, [c_i32, c_p, c_p, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_i32, c_p]),
     "ga_sparta_average_local": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i32, c_i64, c_p, c_i32, c_u64, c_u64, c_f64, c_p,
                                         c_i64, c_f32, c_p, c_p, c_i64, c_p, c_p, c_p]),
-    "ga_sparta_chunk_elems": (c_i64, []),
-    "ga_sparta_mask_chunks": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_p]),
-    "ga_sparta_rows_mean_scatter": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_f32,
-                                            c_p]),
     "ga_demo_tensor_bytes": (c_i32, []),
     "ga_demo_encode": (c_i32, [c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32,
                                c_f32, c_p, c_i64, c_i64, c_p]),
@@ -92,8 +88,6 @@ SIGNATURES = {
     "ga_grad_clip_coef": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "ga_adam_step": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                              c_f32, c_f32, c_f32, c_p, c_p]),
-    "ga_adam_step_select": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
-                                    c_f32, c_f32, c_f32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p]),
 }
 
 _lib = None

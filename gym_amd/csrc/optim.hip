@@ -22,22 +22,10 @@ constexpr int kOptBlock = 256;
 constexpr int64_t kOptChunk = 1024;  // float4 vectors per workgroup
 constexpr int kSumsqBlocks = 1024;   // partials of the norm reduction
 
-// What a SPARTA step needs from the AdamW pass over a [K, ld] rows set
-// (ga_adam_step_select): the packed mask, its per-chunk bases
-// (ga_sparta_mask_chunks; a chunk = one workgroup's 4096 elements) and where the
-// selected elements' updated values go: sel[rep * sel_ld + slot], slot < cap.
-struct SelOut {
-    const uint64_t* bits;
-    const int32_t* chunk_base;
-    float* sel;
-    int64_t sel_ld, cap;
-};
-
-template <bool SEL>
 __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ param, float* __restrict__ grad,
                                                          float* __restrict__ m_, float* __restrict__ v_, int64_t n,
                                                          int64_t ld, AdamParams ap,
-                                                         const float* __restrict__ clip_coef, SelOut so) {
+                                                         const float* __restrict__ clip_coef) {
     const int64_t rep = blockIdx.y;  // replica (simulated node) of a [K, ld] set
     param += rep * ld;
     grad += rep * ld;
@@ -48,32 +36,6 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ par
     const int64_t nv = n >> 2;
     const int64_t lo = (int64_t)blockIdx.x * kOptChunk;
     const int64_t hi = lo + kOptChunk < nv ? lo + kOptChunk : nv;
-    // SEL: the chunk's 64 mask words and the selected count before each (one wave's scan)
-    __shared__ uint64_t sw[SEL ? kOptChunk / 16 : 1];
-    __shared__ int32_t spre[SEL ? kOptChunk / 16 : 1];
-    int64_t sbase = 0;
-    if constexpr (SEL) {
-        static_assert(kOptChunk / 16 == 64, "a chunk's mask words = one wave");
-        if (threadIdx.x < 64) {
-            const int64_t w = (lo >> 4) + threadIdx.x;  // 64-element word of this row
-            uint64_t b = 0;
-            if (w * 64 < n) {
-                b = so.bits[w];
-                if (w * 64 + 64 > n) b &= (1ull << (n - w * 64)) - 1ull;
-            }
-            const int c = __popcll(b);
-            int x = c;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int y = __shfl_up(x, d, 64);
-                if ((int)threadIdx.x >= d) x += y;
-            }
-            sw[threadIdx.x] = b;
-            spre[threadIdx.x] = x - c;
-        }
-        __syncthreads();
-        sbase = so.chunk_base[blockIdx.x];
-    }
     for (int64_t i = lo + threadIdx.x; i < hi; i += kOptBlock) {
         float4 p = stream_load(reinterpret_cast<const float4*>(param) + i);
         float4 g = stream_load(reinterpret_cast<const float4*>(grad) + i);
@@ -88,22 +50,6 @@ __global__ __launch_bounds__(kOptBlock) void adam_kernel(float* __restrict__ par
 #pragma unroll
         for (int e = 0; e < 4; ++e) adam_elem(pp[e], gg[e], mm[e], vv[e], ap);
         const uint32_t o = (uint32_t)(i - lo);
-        if constexpr (SEL) {
-            const int wl = (int)(o >> 4), sh = 4 * (int)(o & 15);  // word in the chunk, bit of element 4i
-            const uint64_t word = sw[wl];
-            uint32_t nib = (uint32_t)(word >> sh) & 0xfu;
-            if (nib) {  // ~2% of lanes at p = 0.005
-                int64_t slot = sbase + spre[wl] + __popcll(word & ((1ull << sh) - 1ull));
-                float* dst = so.sel + rep * so.sel_ld;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if ((nib >> e) & 1u) {
-                        if (slot < so.cap) dst[slot] = pp[e];
-                        ++slot;
-                    }
-                }
-            }
-        }
         store_sc1(reinterpret_cast<float4*>(param) + lo, o, make_float4(pp[0], pp[1], pp[2], pp[3]));
         store_sc1(reinterpret_cast<float4*>(m_) + lo, o, make_float4(mm[0], mm[1], mm[2], mm[3]));
         store_sc1(reinterpret_cast<float4*>(v_) + lo, o, make_float4(vv[0], vv[1], vv[2], vv[3]));
@@ -251,35 +197,9 @@ extern "C" GA_API int ga_adam_step(int dtype, void* param, void* grad, float* ex
     const int64_t nv = n / 4;
     int64_t grid = (nv + kOptChunk - 1) / kOptChunk;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)grid, (unsigned)K), dim3(kOptBlock), 0, stream,
-                       (float*)param, (float*)grad, exp_avg, exp_avg_sq, n, ld, ap, clip_coef, SelOut{});
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)grid, (unsigned)K), dim3(kOptBlock), 0, stream, (float*)param,
+                       (float*)grad, exp_avg, exp_avg_sq, n, ld, ap, clip_coef);
     return check_launch("ga_adam_step");
-}
-
-extern "C" GA_API int ga_adam_step_select(void* param, void* grad, float* exp_avg, float* exp_avg_sq, int64_t K,
-                                          int64_t ld, int64_t n, float lerp_w, float beta2, float one_m_beta2,
-                                          float eps, float wd_factor, float l2_wd, float step_size, float bc2_sqrt,
-                                          const float* clip_coef, const uint64_t* bits, const int32_t* chunk_base,
-                                          float* sel_vals, int64_t sel_ld, int64_t cap, hipStream_t stream) {
-    clear_error();
-    GA_REQUIRE(n >= 0 && K >= 1 && K <= 65535 && cap >= 0, "ga_adam_step_select: bad sizes n=%lld K=%lld",
-               (long long)n, (long long)K);
-    if (n == 0) return GA_OK;
-    GA_REQUIRE(n % 4 == 0, "ga_adam_step_select: n must be a multiple of 4 (arena rows are)");
-    GA_REQUIRE(K == 1 || (ld >= n && ld % 4 == 0), "ga_adam_step_select: ld must be >= n and a multiple of 4");
-    GA_REQUIRE(K == 1 || sel_ld >= cap, "ga_adam_step_select: sel_ld < cap");
-    GA_REQUIRE(param && grad && exp_avg && exp_avg_sq && bits && chunk_base && sel_vals,
-               "ga_adam_step_select: null buffer");
-    GA_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0 &&
-                   (uintptr_t)bits % 8 == 0,
-               "ga_adam_step_select: buffers must be 16-byte aligned (bits 8-byte)");
-    GA_REQUIRE(bc2_sqrt > 0.f, "ga_adam_step_select: bc2_sqrt must be > 0");
-    const AdamParams ap{lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size, bc2_sqrt};
-    const int64_t grid = (n / 4 + kOptChunk - 1) / kOptChunk;
-    hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)grid, (unsigned)K), dim3(kOptBlock), 0, stream,
-                       (float*)param, (float*)grad, exp_avg, exp_avg_sq, n, ld, ap, clip_coef,
-                       SelOut{bits, chunk_base, sel_vals, sel_ld, cap});
-    return check_launch("ga_adam_step_select");
 }
 
 extern "C" GA_API int ga_probe_adam_placement(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,

@@ -828,98 +828,6 @@ __global__ __launch_bounds__(64 * kSpWaves) void sparta_average_rows_wave_kernel
     }
 }
 
-
-// ---- replica-loop SPARTA without the read pass (ga_sparta_mask_chunks,
-// ga_sparta_rows_mean_scatter; the inner AdamW writes the selected values,
-// ga_adam_step_select in optim.hip) -------------------------------------------
-// The [K, ld] rows step used to gather every selected (element, replica) word
-// after the AdamW pass had just streamed it (a random 4-B read per word).  Here
-// the packed mask is indexed first (per 4096-element chunk: the count of
-// selected elements before it), the AdamW kernel -- which streams every row
-// anyway -- writes each selected element's updated value to sel_vals[k][slot],
-// and one kernel sums those K contiguous rows per slot (coalesced) and writes
-// the average back (the only random words left).
-constexpr int kChunkElems = 4096;  // = ga_adam_step's workgroup span (optim.hip kOptChunk float4s)
-constexpr int kChunkWords = kChunkElems / 64;
-static_assert(kChunkWords == 64, "one mask word per lane of a wave");
-
-__device__ __forceinline__ uint64_t mask_word(const uint64_t* bits, int64_t w, int64_t n) {
-    const int64_t e0 = w * 64;
-    if (e0 >= n) return 0ull;
-    const uint64_t b = bits[w];
-    return e0 + 64 <= n ? b : b & ((1ull << (n - e0)) - 1ull);
-}
-
-// one wave per chunk: counts[c] = selected elements of chunk c
-__global__ __launch_bounds__(256) void sparta_chunk_count_kernel(const uint64_t* __restrict__ bits, int64_t n,
-                                                                 int64_t nchunks, int32_t* __restrict__ counts) {
-    const int lane = threadIdx.x & 63;
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= nchunks) return;
-    int v = __popcll(mask_word(bits, c * kChunkWords + lane, n));
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-    if (lane == 0) counts[c] = v;
-}
-
-// one wave per chunk: its selected elements listed in LDS (ascending), then one
-// lane per listed element sums sel_vals[k][slot] over k = 0 .. K-1 in ascending
-// order from 0 (the rows kernel's fp32 order: bit-identical), divides, and
-// writes the average to the element of every replica row
-template <typename T>
-__global__ __launch_bounds__(64 * kSpWaves) void sparta_rows_mean_scatter_kernel(
-    T* src, int64_t K, int64_t ld, int64_t n, const uint64_t* __restrict__ bits, const int32_t* __restrict__ chunk_base,
-    const float* __restrict__ sel_vals, int64_t sel_ld, int64_t cap, float divisor) {
-    __shared__ uint16_t lists[kSpWaves][kWList];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint16_t* list = lists[wid];
-    const int64_t c = (int64_t)blockIdx.x * kSpWaves + wid;
-    if (c * kChunkElems >= n) return;  // wave-uniform; the waves never meet at a barrier
-    const uint64_t b0 = mask_word(bits, c * kChunkWords + lane, n);
-    const int cnt = __popcll(b0);
-    int x = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    const int total = __shfl(x, 63, 64);
-    const int local0 = x - cnt;
-    const int64_t base = chunk_base[c];
-    for (int w0 = 0; w0 < total; w0 += kWList) {  // one window unless p is large
-        {
-            int l = local0;
-            uint64_t b = b0;
-            while (b) {
-                const int j = __builtin_ctzll(b);
-                b &= b - 1;
-                if (l >= w0 && l < w0 + kWList) list[l - w0] = (uint16_t)(lane * 64 + j);
-                ++l;
-            }
-        }
-        wave_sync();
-        const int wtot = (total - w0) < kWList ? (total - w0) : kWList;
-        for (int e0 = 0; e0 < wtot; e0 += 64) {
-            const int64_t slot = base + w0 + e0 + lane;
-            const bool on = e0 + lane < wtot && slot < cap;
-            T* p = src + c * kChunkElems + (on ? list[e0 + lane] : 0);
-            float acc = 0.f;
-            for (int64_t k0 = 0; k0 < K; k0 += kRowsKB) {
-                float v[kRowsKB];
-#pragma unroll
-                for (int u = 0; u < kRowsKB; ++u) v[u] = on && k0 + u < K ? sel_vals[(k0 + u) * sel_ld + slot] : 0.f;
-#pragma unroll
-                for (int u = 0; u < kRowsKB; ++u)
-                    if (k0 + u < K) acc += v[u];
-            }
-            const float avg = acc / divisor;
-            if (on)
-                for (int64_t k = 0; k < K; ++k) Elem<T>::store(p + k * ld, avg);
-        }
-        wave_sync();  // the list is rewritten by the next window
-    }
-}
-
 template <typename T>
 static bool launch_average_rows_wave(hipStream_t stream, const Pred& P, int64_t n, void* src, int64_t ld, int64_t K,
                                      float divisor) {
@@ -1471,52 +1379,4 @@ extern "C" GA_API int ga_sparta_scatter(int dtype, const void* vals, const int32
         default: set_error("ga_sparta_scatter: unknown dtype %d", dtype); return GA_EINVAL;
     }
     return check_launch("ga_sparta_scatter");
-}
-
-extern "C" GA_API int64_t ga_sparta_chunk_elems(void) { return kChunkElems; }
-
-extern "C" GA_API int ga_sparta_mask_chunks(const uint64_t* bits, int64_t n, int32_t* chunk_base, int64_t cap,
-                                            int64_t* count, hipStream_t stream) {
-    clear_error();
-    GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX && cap >= 0, "ga_sparta_mask_chunks: bad n=%lld cap=%lld",
-               (long long)n, (long long)cap);
-    GA_REQUIRE(count, "ga_sparta_mask_chunks: null count");
-    if (n == 0) return hipMemsetAsync(count, 0, 2 * sizeof(int64_t), stream) == hipSuccess ? GA_OK : GA_EHIP;
-    GA_REQUIRE(bits && chunk_base && ((uintptr_t)bits % 8) == 0, "ga_sparta_mask_chunks: null/misaligned buffer");
-    const int64_t nchunks = ceil_div(n, (int64_t)kChunkElems);
-    hipLaunchKernelGGL(sparta_chunk_count_kernel, dim3((unsigned)ceil_div(nchunks, (int64_t)4)), dim3(256), 0, stream,
-                       bits, n, nchunks, chunk_base);
-    if (int e = check_launch("ga_sparta_mask_chunks (count)")) return e;
-    // in place: every pass of the scan reads its counts into LDS before it writes offsets
-    hipLaunchKernelGGL(sparta_scan_kernel, dim3(1), dim3(kScanBlock), 0, stream, chunk_base, nchunks, chunk_base, cap,
-                       count);
-    return check_launch("ga_sparta_mask_chunks (scan)");
-}
-
-extern "C" GA_API int ga_sparta_rows_mean_scatter(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
-                                                  const uint64_t* bits, const int32_t* chunk_base,
-                                                  const float* sel_vals, int64_t sel_ld, int64_t cap, float divisor,
-                                                  hipStream_t stream) {
-    clear_error();
-    GA_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX && K >= 1 && cap >= 0, "ga_sparta_rows_mean_scatter: bad sizes");
-    GA_REQUIRE(K == 1 || ld >= n, "ga_sparta_rows_mean_scatter: ld < n");
-    GA_REQUIRE(K == 1 || sel_ld >= cap, "ga_sparta_rows_mean_scatter: sel_ld < cap");
-    GA_REQUIRE(divisor > 0.0f, "ga_sparta_rows_mean_scatter: divisor must be > 0");
-    if (n == 0 || cap == 0) return GA_OK;
-    GA_REQUIRE(reps && bits && chunk_base && sel_vals && ((uintptr_t)bits % 8) == 0,
-               "ga_sparta_rows_mean_scatter: null/misaligned buffer");
-    const int64_t nchunks = ceil_div(n, (int64_t)kChunkElems);
-    const dim3 grid((unsigned)ceil_div(nchunks, (int64_t)kSpWaves)), block(64 * kSpWaves);
-    switch (dtype) {
-        case GA_F32:
-            hipLaunchKernelGGL(sparta_rows_mean_scatter_kernel<float>, grid, block, 0, stream, (float*)reps, K, ld, n,
-                               bits, chunk_base, sel_vals, sel_ld, cap, divisor);
-            break;
-        case GA_BF16:
-            hipLaunchKernelGGL(sparta_rows_mean_scatter_kernel<__hip_bfloat16>, grid, block, 0, stream,
-                               (__hip_bfloat16*)reps, K, ld, n, bits, chunk_base, sel_vals, sel_ld, cap, divisor);
-            break;
-        default: set_error("ga_sparta_rows_mean_scatter: unknown dtype %d", dtype); return GA_EINVAL;
-    }
-    return check_launch("ga_sparta_rows_mean_scatter");
 }

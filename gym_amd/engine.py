@@ -403,45 +403,15 @@ class Sparta:
         self.coll.all_reduce_(self.vals[:cap_used])
         ops.sparta_scatter(self.vals, self.idx, self.count, cap_used, float(self.K_total), reps, layout=self.layout)
         if mask is None or mask_cap is not None:  # overflow flag read back asynchronously, checked next step
-            self._record_flag()
-
-    def _record_flag(self):
-        hb = self._flag_host[self._flag_slot]
-        self._flag_slot ^= 1
-        hb.copy_(self.count, non_blocking=True)
-        if self.device.type == "cuda":
-            ev = torch.cuda.Event()
-            ev.record()
-            self._pending.append((ev, hb))
-        elif int(hb[1]) != 0:
-            raise RuntimeError(f"SPARTA: {int(hb[0])} elements selected > capacity {self.cap}")
-
-    # ---- the replica loop's step on the [K, ld] rows set, with the inner AdamW --------
-    def rows_begin(self, bits):
-        """Index the packed mask `bits` (rank-local, no exchange) by 4096-element
-        chunk and return the ops.RowsSelect the inner AdamW (ArenaAdam.step(
-        select=...), ga_adam_step_select) fills with every selected element's
-        updated value per replica; rows_finish then averages them.  Replaces the
-        gather of the rows pass: the AdamW kernel already streams every row
-        (communicate_optimize_strategy.py:67-85 + sparta.py:24-44 for K nodes)."""
-        if self.coll.exchange or self.layout != "rows":
-            raise ValueError("Sparta.rows_begin: a single-process [K, ld] rows step")
-        if getattr(self, "_rows_sel", None) is None or self._rows_sel.cap != self.cap:
-            cb = torch.empty(ops.sparta_chunk_count(self.n), dtype=torch.int32, device=self.device)
-            sv = torch.empty(self.K_local, self.cap, dtype=torch.float32, device=self.device)
-            self._rows_sel = ops.RowsSelect(None, cb, sv, self.cap)
-        self._poll(1)
-        sel = self._rows_sel
-        sel.bits = bits
-        ops.sparta_mask_chunks(bits, self.n, sel.chunk_base, sel.cap, self.count)
-        return sel
-
-    def rows_finish(self, reps, sel):
-        """Every selected element of every replica row <- the ascending-replica
-        sum of the values the AdamW pass wrote / K (ga_sparta_rows_mean_scatter);
-        the capacity flag is read back asynchronously, as in __call__."""
-        ops.sparta_rows_mean_scatter(reps, self.n, sel, float(self.K_total))
-        self._record_flag()
+            hb = self._flag_host[self._flag_slot]
+            self._flag_slot ^= 1
+            hb.copy_(self.count, non_blocking=True)
+            if self.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+                self._pending.append((ev, hb))
+            elif int(hb[1]) != 0:
+                raise RuntimeError(f"SPARTA: {int(hb[0])} elements selected > capacity {self.cap}")
 
 
 class DeMoCodec:

@@ -274,16 +274,8 @@ class ArenaAdam(torch.optim.Optimizer):
                 out.append([o, o + n])
         return [(a, b) for a, b in out]
 
-    def can_select(self):
-        """Whether step(select=...) can run now: every parameter has a gradient
-        (whole rows, so the kernel's workgroups are the mask's 4096-element chunks)."""
-        return all(self._ranges(k) == [(0, self.ld)] for k in range(self.K)) and self.ld % 4 == 0
-
     @torch.no_grad()
-    def step(self, closure=None, max_norm=None, select=None):
-        """select: an ops.RowsSelect (gym_amd.engine.Sparta.rows_begin): the same
-        step also writes SPARTA's selected values (ga_adam_step_select); needs
-        can_select()."""
+    def step(self, closure=None, max_norm=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -307,18 +299,8 @@ class ArenaAdam(torch.optim.Optimizer):
         if max_norm:
             ops.grad_clip_coef(self.G, self.ld, max_norm, self._partials, self._clip)
             clip = self._clip
-        full = all(r == [(0, self.ld)] for r in ranges)
-        if select is not None and not full:
-            raise ValueError("ArenaAdam.step(select=...): every parameter needs a gradient (can_select())")
-        if self._M is not None and full:
-            if select is not None:
-                hp["select"] = select
+        if self._M is not None and all(r == [(0, self.ld)] for r in ranges):
             ops.adam_step(self.P, self.G, self._M, self._V, clip_coef=clip, **hp)
-            return loss
-        if select is not None:  # moments placed per replica: one launch per replica
-            for k in range(self.K):
-                ck = clip[2 * k:2 * k + 2] if clip is not None else None
-                ops.adam_step(self.P[k], self.G[k], self._Mr[k], self._Vr[k], clip_coef=ck, select=select.row(k), **hp)
             return loss
         for k in range(self.K):  # per replica (its moments placed apart, or partial ranges)
             ck = clip[2 * k:2 * k + 2] if clip is not None else None

@@ -300,58 +300,6 @@ def sparta_scatter(vals, idx, count, cap, divisor, dst, layout="rows"):
                                   _p(dst2), K, ld, code, _stream()), "ga_sparta_scatter")
 
 
-def sparta_chunk_elems():
-    """Elements per chunk of ga_sparta_mask_chunks (= one ga_adam_step workgroup)."""
-    return int(lib().ga_sparta_chunk_elems())
-
-
-def sparta_chunk_count(n):
-    """int32 entries of the chunk_base buffer for n elements."""
-    e = sparta_chunk_elems()
-    return (int(n) + e - 1) // e
-
-
-class RowsSelect:
-    """What ga_adam_step_select needs for one replica-loop SPARTA step: the
-    packed mask, its chunk bases (sparta_mask_chunks), the [K, sel_ld] buffer
-    of the selected values and its capacity."""
-
-    def __init__(self, bits, chunk_base, sel_vals, cap):
-        self.bits, self.chunk_base, self.sel_vals, self.cap = bits, chunk_base, sel_vals, int(cap)
-
-    def row(self, k):
-        """The same for replica k alone (a per-replica AdamW launch)."""
-        return RowsSelect(self.bits, self.chunk_base, self.sel_vals[k:k + 1], self.cap)
-
-
-def sparta_mask_chunks(bits, n, chunk_base, cap, count):
-    """chunk_base[c] = selected elements of the packed mask before 4096-element
-    chunk c; count = (total, total > cap)."""
-    _gpu(bits, chunk_base, count)
-    if bits.dtype != torch.int64 or bits.numel() < sparta_mask_words(n):
-        raise ValueError("sparta_mask_chunks: bits must be int64 words covering n elements")
-    if chunk_base.dtype != torch.int32 or chunk_base.numel() < sparta_chunk_count(n):
-        raise ValueError("sparta_mask_chunks: chunk_base must hold sparta_chunk_count(n) int32")
-    if count.dtype != torch.int64 or count.numel() < 2:
-        raise ValueError("sparta_mask_chunks: count must be int64[2]")
-    check(lib().ga_sparta_mask_chunks(_p(bits), int(n), _p(chunk_base), int(cap), _p(count), _stream()),
-          "ga_sparta_mask_chunks")
-
-
-def sparta_rows_mean_scatter(reps, n, sel, divisor):
-    """Every selected element of the [K, ld] rows set <- the ascending-replica
-    sum of its K values in sel.sel_vals / divisor (RowsSelect sel)."""
-    r2 = _as2d(reps)
-    _gpu(r2, sel.bits, sel.chunk_base, sel.sel_vals)
-    K, ld = _rows_ld(r2)
-    sv = sel.sel_vals
-    if sv.dtype != torch.float32 or sv.dim() != 2 or sv.shape[0] != K or sv.shape[1] < sel.cap or sv.stride(1) != 1:
-        raise ValueError("sparta_rows_mean_scatter: sel_vals must be fp32 [K, >= cap]")
-    check(lib().ga_sparta_rows_mean_scatter(_dtype_code(r2), _p(r2), K, ld, int(n), _p(sel.bits),
-                                            _p(sel.chunk_base), _p(sv), sv.stride(0), sel.cap, float(divisor),
-                                            _stream()), "ga_sparta_rows_mean_scatter")
-
-
 def demo_encode(plan, param, grad, delta, payload, lr, decay, wd_factor):
     """plan: gym_amd.demo_codec.DemoPlan.  param/grad/delta: [K, ld] replica sets
     (or 1-D); payload: int32 [K, 2*M]."""
@@ -494,7 +442,7 @@ def grad_clip_coef(grad, n, max_norm, partials, out):
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps, wd_factor, l2_wd, step_size,
-              bc2_sqrt, clip_coef=None, n=None, select=None):
+              bc2_sqrt, clip_coef=None, n=None):
     """One fused Adam/AdamW step over fp32 [K, ld] replica sets (or 1-D buffers)
     of one shape; every replica's first n elements (see include/gym_amd.h)."""
     ts = [_as2d(t) for t in (param, grad, exp_avg, exp_avg_sq)]
@@ -506,18 +454,6 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, lerp_w, beta2, one_m_beta2, eps,
     n = ts[0].shape[1] if n is None else int(n)
     if clip_coef is not None and clip_coef.numel() < 2 * K:
         raise ValueError("adam_step: clip_coef must hold 2 floats per replica")
-    if select is not None:  # SPARTA's selected values written by the same pass (ga_adam_step_select)
-        sv = select.sel_vals
-        _gpu(select.bits, select.chunk_base, sv)
-        if sv.dtype != torch.float32 or sv.dim() != 2 or sv.shape[0] != K or sv.shape[1] < select.cap \
-                or sv.stride(1) != 1:
-            raise ValueError("adam_step: select.sel_vals must be fp32 [K, >= cap]")
-        check(lib().ga_adam_step_select(_p(ts[0]), _p(ts[1]), _p(ts[2]), _p(ts[3]), K, ld, n, float(lerp_w),
-                                        float(beta2), float(one_m_beta2), float(eps), float(wd_factor), float(l2_wd),
-                                        float(step_size), float(bc2_sqrt), _p(clip_coef), _p(select.bits),
-                                        _p(select.chunk_base), _p(sv), sv.stride(0), select.cap, _stream()),
-              "ga_adam_step_select")
-        return
     check(lib().ga_adam_step(_GA_F32, _p(ts[0]), _p(ts[1]), _p(ts[2]), _p(ts[3]), K, ld, n, float(lerp_w),
                              float(beta2), float(one_m_beta2), float(eps), float(wd_factor), float(l2_wd),
                              float(step_size), float(bc2_sqrt), _p(clip_coef), _stream()), "ga_adam_step")

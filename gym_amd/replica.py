@@ -186,16 +186,6 @@ class ReplicaRunner:
             if s.local_step % s.H == 0 and s.local_step > 0:
                 self.outer(P)
         elif isinstance(s, SPARTAStrategy):
-            if not self.philox and self._rows_fused():
-                # the mask first (nothing between the inner step and the draw uses the
-                # generator), indexed; the AdamW pass writes the selected values; then
-                # one kernel averages them into every row (no read pass over the rows)
-                sel = self.sparta.rows_begin(self._build_bits())
-                self.optim.step(max_norm=self.max_norm or None, select=sel)
-                self.sparta.rows_finish(P, sel)
-                self.iteration += 1
-                self._after_step()
-                return
             self._inner()
             if self.philox:
                 self.sparta(P, seed=self.seed, iteration=self.iteration, skip=self._skip_table())
@@ -212,10 +202,6 @@ class ReplicaRunner:
                     self._island_average(P)
                 else:
                     self.mean(P)
-        self._after_step()
-
-    def _after_step(self):
-        s = self.s
         for sch in self.lr_scheds:
             sch.step()
         if self.rank == 0 and self.lr_scheds:
@@ -268,23 +254,6 @@ class ReplicaRunner:
             ops.replica_mean(src, self._isl_row, rows=rows, divisor=float(len(members)))
             for m in mine:
                 ops.replica_mean(self._isl_row, P[m - lo:m - lo + 1], divisor=1.0)
-
-    def _rows_fused(self):
-        """SPARTA with the reference's RandomIndexSelector (capacity bound known),
-        one process, the fused AdamW over whole rows: the read-free step."""
-        return (not self.coll.exchange and type(self.s.index_selector) is RandomIndexSelector
-                and isinstance(self.optim, ArenaAdam) and self.ra.device.type == "cuda"
-                and self.ra.dtype == torch.float32 and self.optim.can_select())
-
-    def _build_bits(self):
-        """Node 0's masks (the reference draw) as packed words (the fused draw writes
-        them; the per-tensor torch fallback fills the uint8 arena, packed here)."""
-        a0 = self.ra.arenas[0]
-        packed = draw_masks(self.s.index_selector, a0.params, self.ra.layout.views(self.mask), set(self._grad_less()),
-                            self.iteration, self.draw, bits=self.bits, coll=self.coll, defer=False)
-        if packed is None:
-            ops.sparta_pack_mask(self.mask, self.ra.ld, self.bits)
-        return self.bits
 
     def _grad_less(self):
         """Indices of node 0's tensors without a gradient (skipped, sparta.py:29-30)."""

@@ -293,32 +293,6 @@ GA_API int ga_sparta_average_local(int dtype, void* reps, int64_t K, int64_t ld,
                                    float divisor, int32_t* idx, void* vals,
                                    int64_t cap, int64_t* count, void* work, hipStream_t stream);
 
-/*
- * Replica-loop SPARTA without a read pass over the rows (three calls; the
- * reference's sparta.py:24-44 for K nodes of one process on a [K, ld] set):
- *   1. ga_sparta_mask_chunks: per ga_sparta_chunk_elems() = 4096-element chunk
- *      of the packed mask `bits` (bit j of word w = element 64w + j; n elements),
- *      chunk_base[c] = selected elements before chunk c (int32, ceil(n/4096)
- *      entries), count[0] = total, count[1] = total > cap.
- *   2. ga_adam_step_select (below): the inner AdamW step, which also writes each
- *      selected element's updated value of replica k to sel_vals[k*sel_ld + slot]
- *      (slot = its rank among the selected, < cap).
- *   3. ga_sparta_rows_mean_scatter: for each selected element, the sum over
- *      k = 0..K-1 of sel_vals[k*sel_ld + slot] in ascending k from 0 (fp32) /
- *      divisor, written to that element of every replica row of `reps`
- *      ([K, ld]; the same value ga_sparta_average_local writes).
- * Replaces: the mask gather `param.data[mask]` (sparta.py:38) -- the values come
- * out of the optimizer pass that streams the rows anyway -- and the all-reduce
- * + divide + masked_scatter_ (sparta.py:39-42) for nodes of one process.
- */
-GA_API int64_t ga_sparta_chunk_elems(void);
-GA_API int ga_sparta_mask_chunks(const uint64_t* bits, int64_t n, int32_t* chunk_base, int64_t cap,
-                                 int64_t* count, hipStream_t stream);
-GA_API int ga_sparta_rows_mean_scatter(int dtype, void* reps, int64_t K, int64_t ld, int64_t n,
-                                       const uint64_t* bits, const int32_t* chunk_base,
-                                       const float* sel_vals, int64_t sel_ld, int64_t cap, float divisor,
-                                       hipStream_t stream);
-
 /* ---- DeMo DCT codec ------------------------------------------------------ */
 
 /*
@@ -460,20 +434,6 @@ GA_API int ga_adam_step(int dtype, void* param, void* grad, float* exp_avg, floa
                         int64_t ld, int64_t n, float lerp_w, float beta2, float one_m_beta2, float eps,
                         float wd_factor, float l2_wd, float step_size, float bc2_sqrt, const float* clip_coef,
                         hipStream_t stream);
-
-/*
- * ga_adam_step (fp32, n % 4 == 0) that also hands SPARTA its selected values:
- * for every element selected in `bits` (indexed by ga_sparta_mask_chunks into
- * chunk_base), replica k's updated parameter goes to sel_vals[k*sel_ld + slot]
- * (slot < cap).  Same parameter / moment results as ga_adam_step.  Replaces
- * `self.optim.step()` + the gather `param.data[mask]` of one SPARTA step
- * (communicate_optimize_strategy.py:67-85, sparta.py:38).
- */
-GA_API int ga_adam_step_select(void* param, void* grad, float* exp_avg, float* exp_avg_sq, int64_t K, int64_t ld,
-                               int64_t n, float lerp_w, float beta2, float one_m_beta2, float eps, float wd_factor,
-                               float l2_wd, float step_size, float bc2_sqrt, const float* clip_coef,
-                               const uint64_t* bits, const int32_t* chunk_base, float* sel_vals, int64_t sel_ld,
-                               int64_t cap, hipStream_t stream);
 
 #ifdef __cplusplus
 }
