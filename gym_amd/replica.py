@@ -245,12 +245,16 @@ class ReplicaRunner:
             self.coll.all_gather_into(self._isl_all.view(-1), P.reshape(-1))
             src = self._isl_all
         lo, hi = self.first_node, self.first_node + self.K
-        for i in range(0, N, s):
-            members = sorted(ranks[i:i + s])
+        islands = [sorted(ranks[i:i + s]) for i in range(0, N, s)]
+        # every island's ascending member list in ONE host-to-device copy per round
+        table = torch.tensor([m for isl in islands for m in isl], dtype=torch.int32).to(P.device, non_blocking=True)
+        a = 0
+        for members in islands:
+            rows = table[a:a + len(members)]
+            a += len(members)
             mine = [m for m in members if lo <= m < hi]
             if not mine:
                 continue
-            rows = torch.tensor(members, dtype=torch.int32, device=P.device)
             ops.replica_mean(src, self._isl_row, rows=rows, divisor=float(len(members)))
             for m in mine:
                 ops.replica_mean(self._isl_row, P[m - lo:m - lo + 1], divisor=1.0)
