@@ -16,6 +16,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gym_amd.h")
 
 GA_F32 = 0
 GA_BF16 = 1
+GA_BF16_REF = 2  # DeMo entry points: bf16 arenas, the reference's bf16 arithmetic
 GA_LAYOUT_ROWS = 0
 GA_LAYOUT_ELEM_MAJOR = 1
 GA_MASK_BYTES = 0

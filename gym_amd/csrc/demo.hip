@@ -119,6 +119,15 @@ __device__ __forceinline__ f32x16 mm64(const float* A, const float* Bm, int tid)
 #define TILE_ROW kLd, 1      // a 64x65 LDS tile, or the LDS basis F, read by rows
 #define TILE_COL 1, kLd      // the same, transposed (F^T)
 #define GTAB_COL 1, 64       // a 64x64 global table, transposed
+#define GTAB_ROW 64, 1       // a 64x64 global table, by rows
+
+// GA_BF16_REF: the reference's bf16 arithmetic (demo.py:235-236, 238-252 as torch
+// runs it): every stage of a transform rounds to bf16 (nearest even)
+__device__ __forceinline__ float bf16r(float v) { return __bfloat162float(__float2bfloat16(v)); }
+__device__ __forceinline__ void round16(f32x16& a) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[r] = bf16r(a[r]);
+}
 
 // Row / column of accumulator register r for this lane (C/D layout of the 32x32 MFMA).
 __device__ __forceinline__ int acc_row(int r, int tid) {
@@ -134,6 +143,29 @@ __device__ __forceinline__ void store_acc(float* tile, const f32x16& acc, int ti
     const int c = acc_col(tid);
 #pragma unroll
     for (int r = 0; r < 16; ++r) tile[acc_row(r, tid) * kLd + c] = acc[r];
+}
+
+// The reference's decode of a coefficient tile S (natural layout, LDS) in bf16
+// stages: Z = bf16(F1 . S) (einsum_2d_t contracts the coefficient rows first,
+// B1[k][b] = F1[b][k]), then R = bf16(Z . F2^T); n1 == 1: one stage (the 1-D
+// einsum_2d_t).  F1 from the LDS basis (f1 = 0: F1 == F2), the global DCT table
+// (f1 = 1: tab1 = F1, row-major) or the inverse table (f1 = 2: tab1 = B1 = F1^T).
+// Leaves R in S (natural layout); barriers inside.
+__device__ __forceinline__ void ref_inverse(float* S, const float* FT, const float* tab1, int f1, int n1, int tid) {
+    f32x16 acc;
+    if (n1 > 1) {
+        acc = f1 == 0 ? mm64<TILE_ROW, TILE_ROW>(FT, S, tid)
+                      : (f1 == 1 ? mm64<GTAB_ROW, TILE_ROW>(tab1, S, tid) : mm64<GTAB_COL, TILE_ROW>(tab1, S, tid));
+        round16(acc);
+        LDS_BARRIER();
+        store_acc(S, acc, tid);
+        LDS_BARRIER();
+    }
+    acc = mm64<TILE_ROW, TILE_COL>(S, FT, tid);  // . F2^T
+    round16(acc);
+    LDS_BARRIER();
+    store_acc(S, acc, tid);
+    LDS_BARRIER();
 }
 
 // ---- DCT symmetry (64-point bases): F[63-i][k] = (-1)^k F[i][k] ----
@@ -674,7 +706,11 @@ __device__ __forceinline__ const uint32_t* topk_emit(const f32x16& y, const Perm
 
 
 constexpr int kDmEncWaves = 3;  // workgroups per CU the encode is compiled for (register budget ~168 VGPRs, no spills)
-template <typename T>
+// REF (T = bf16): the reference's bf16 arithmetic (GA_BF16_REF): delta rounded after
+// the decay and after the gradient add, Y = bf16(bf16(F1^T X) F2) (rows first, as the
+// reference's einsum contracts), the residual as its bf16 two-stage decode
+// (ref_inverse), bf16 bases from the caller's table; no symmetric folding.
+template <typename T, bool REF = false>
 __global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const float* __restrict__ F, T* param,
     const T* __restrict__ grad, T* delta, int64_t ld, float lr, float decay, float wd_factor, int32_t* payload,
@@ -740,8 +776,15 @@ __global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) x[i][e] = fmaf(lr, g[i][e], decay != 1.f ? d[i][e] * decay : d[i][e]);
-        const bool sym = n2 == 64 && (n1 == 64 || n1 == 1);  // uniform
+            for (int e = 0; e < 4; ++e) {
+                if (REF) {  // delta.mul_(decay) then delta.add_(grad, alpha=lr), each a bf16 tensor op
+                    const float d1 = decay != 1.f ? bf16r(d[i][e] * decay) : d[i][e];
+                    x[i][e] = bf16r(fmaf(lr, g[i][e], d1));
+                } else {
+                    x[i][e] = fmaf(lr, g[i][e], decay != 1.f ? d[i][e] * decay : d[i][e]);
+                }
+            }
+        const bool sym = !REF && n2 == 64 && (n1 == 64 || n1 == 1);  // uniform
         if (sym) put_tile_sym(X, io, x);
         else put_tile(X, io, x);
         // prefetch the next chunk's delta and grad (in flight until the next iteration)
@@ -762,6 +805,20 @@ __global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
 
         // 2. Y = F1^T . X . F2 on the matrix cores (half the MFMAs for 64-point bases)
         f32x16 acc;
+        if (REF) {  // U = bf16(F1^T . X) (the chunk rows first), Y = bf16(U . F2)
+            const int tid = opaque_tid();
+            if (n1 > 1) {
+                acc = td.basis1 == td.basis2 ? mm64<TILE_COL, TILE_ROW>(FT, X, tid)
+                                             : mm64<GTAB_COL, TILE_ROW>(F + (int64_t)td.basis1 * 4096, X, tid);
+                round16(acc);
+                LDS_BARRIER();
+                store_acc(X, acc, tid);
+                LDS_BARRIER();
+            }
+            acc = mm64<TILE_ROW, TILE_ROW>(X, FT, tid);
+            round16(acc);
+            GA_PH(1);
+        } else {
         {
             const int tid = opaque_tid();  // a fresh lane id per phase keeps its derived values short-lived
         if (sym) {
@@ -782,6 +839,7 @@ __global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
             else acc = mm64<GTAB_COL, TILE_ROW>(F + (int64_t)td.basis1 * 4096, X, tid);
         }  // n1 == 1: F1 = [1], Y = T
         }
+        }
         GA_PH(2);
         Perm P;
         P.tid = opaque_tid();
@@ -801,7 +859,19 @@ __global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
         const bool split = P.rowp && ent == cand;  // uniform
         f32x16 R;
         const int tid4 = opaque_tid();
-        if (split) {
+        if (REF) {
+            // the reference's transmit_grad: decompress (the k entries into a zero tile), then
+            // its bf16 two-stage decode (demo.py:174-180); R is left in X
+            LDS_BARRIER();  // every wave is done with its top-k reads of X
+            for (int q = tid4; q < kTile; q += kDmBlock) X[q] = 0.f;
+            LDS_BARRIER();
+            for (int j = tid4; j < k; j += kDmBlock) {
+                const uint32_t pos = ent[2 * j];
+                X[(pos >> 6) * kLd + (pos & 63)] = __uint_as_float(ent[2 * j + 1]);
+            }
+            LDS_BARRIER();
+            ref_inverse(X, FT, F + (int64_t)td.basis1 * 4096, td.basis1 == td.basis2 ? 0 : 1, n1, tid4);
+        } else if (split) {
             const int tid = tid4;
             const int lane = tid & 63, par = tid >> 7;
             uint32_t* own = lst + 256 * (tid >> 6);
@@ -828,8 +898,10 @@ __global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
         } else {
             R = sparse_synth(ent, k, FT, basis1_of(td, F, false), -1, tid4);
         }
-        store_acc(X, R, tid4);  // X is free: every wave is past its last read of T (top-k barriers)
-        LDS_BARRIER();
+        if (!REF) {
+            store_acc(X, R, tid4);  // X is free: every wave is past its last read of T (top-k barriers)
+            LDS_BARRIER();
+        }
         GA_PH(4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -865,7 +937,9 @@ __global__ __launch_bounds__(kDmBlock, kDmEncWaves) void demo_encode_kernel(
 // nsrc > 1: node-ordered scatter-mean into the tile, then two dense products.
 constexpr int kPfSrc = 8;  // sources whose entries are prefetched into registers (k <= 256)
 
-template <typename T, typename CntT>
+// REF (T = bf16): the reference's bf16 decode (GA_BF16_REF): the scatter-mean
+// rounded to bf16, then its two-stage bf16 inverse (ref_inverse), also for one source.
+template <typename T, typename CntT, bool REF = false>
 __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_decode_kernel(
     const ga_demo_tensor* __restrict__ tens, int ntens, int nchunks, const float* __restrict__ B,
     const int32_t* __restrict__ payload, int64_t pstride, int64_t M, int nsrc, T* param, T* grad, int64_t K,
@@ -916,7 +990,7 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
         const int64_t eoff = td.payload_off + (int64_t)c * nk;
         f32x16 acc;
         // the dense (several-source) inverse uses the DCT symmetry for 64-point bases
-        const bool dsym = nsrc > 1 && n2 == 64 && (n1 == 64 || n1 == 1);  // uniform
+        const bool dsym = !REF && nsrc > 1 && n2 == 64 && (n1 == 64 || n1 == 1);  // uniform
         const int next = chunk + (int)gridDim.x;
         const bool more = next < nchunks;
         int tixn = tix;
@@ -925,7 +999,7 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
             tixn = advance_tensor(tens, ntens, tix, next, tid);
             tdn = tens[tixn];
         }
-        if (nsrc == 1) {
+        if (nsrc == 1 && !REF) {
             // entry list (b*64 + d, value) straight from the payload
             for (int j = tid; j < nk; j += kDmBlock) {
                 const int x = use_pf ? pidx[0] : payload[eoff + j];
@@ -972,8 +1046,11 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
             for (int e = tid; e < 4096; e += kDmBlock) {
                 const int n = cnt[e];
                 if (n > 1) S[(e >> 6) * kLd + (e & 63)] /= (float)n;
+                if (REF) S[(e >> 6) * kLd + (e & 63)] = bf16r(S[(e >> 6) * kLd + (e & 63)]);
             }
             LDS_BARRIER();
+            if (REF) ref_inverse(S, FT, B + (int64_t)td.basis1 * 4096, td.basis1 == td.basis2 ? 0 : 2, n1, tid);
+            if (!REF) {
             // g = B1^T . S . B2 = F1 . S . F2^T on the matrix cores, in place in S
             // (half the MFMAs for 64-point bases: mm_isym1 / mm_isym2)
             acc = dsym ? mm_isym1(S, FT, tid) : mm64<TILE_ROW, TILE_COL>(S, FT, tid);  // U = S . F2^T
@@ -986,10 +1063,12 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
                 else acc = mm64<GTAB_COL, TILE_ROW>(B + (int64_t)td.basis1 * 4096, S, tid);  // F1[i][k] = B1[k][i]
                 LDS_BARRIER();
             }
+            }  // !REF
         }
-        store_acc(S, acc, tid);
-        LDS_BARRIER();
-
+        if (!REF) {  // REF: ref_inverse left g in S
+            store_acc(S, acc, tid);
+            LDS_BARRIER();
+        }
         // grad = sign(g) (torch.sign: NaN -> 0);  p -= lr * grad   (demo.py:200-209)
         float p1[4][4];
         ChunkIO ion = io;
@@ -1062,23 +1141,23 @@ static int check_tensors_host(int32_t ntensors, int32_t nchunks) {
     return GA_OK;
 }
 
-template <typename T>
+template <typename T, bool REF = false>
 static void launch_encode(const ga_demo_tensor* tensors, int32_t ntensors, int32_t nchunks, const float* F,
                           void* param, const void* grad, void* delta, int64_t K, int64_t ld, float lr, float decay,
                           float wd_factor, int32_t* payload, int64_t pstride, int64_t M, int ptr_vec,
                           hipStream_t stream) {
-    auto kern = demo_encode_kernel<T>;
+    auto kern = demo_encode_kernel<T, REF>;
     static const int resident = resident_blocks(kern);
     hipLaunchKernelGGL(kern, persistent_grid(resident, nchunks, K), dim3(kDmBlock), 0, stream, tensors, ntensors,
                        nchunks, F, (T*)param, (const T*)grad, (T*)delta, ld, lr, decay, wd_factor, payload, pstride,
                        M, ptr_vec);
 }
 
-template <typename T, typename CntT>
+template <typename T, typename CntT, bool REF = false>
 static void launch_decode(const ga_demo_tensor* tensors, int32_t ntensors, int32_t nchunks, const float* B,
                           const int32_t* payload, int64_t pstride, int64_t M, int64_t S, void* param, void* grad,
                           int64_t K, int64_t ld, float lr, int ptr_vec, hipStream_t stream) {
-    auto kern = demo_decode_kernel<T, CntT>;
+    auto kern = demo_decode_kernel<T, CntT, REF>;
     static const int resident = resident_blocks(kern);
     hipLaunchKernelGGL(kern, persistent_grid(resident, nchunks, 1), dim3(kDmBlock), 0, stream, tensors, ntensors,
                        nchunks, B, payload, pstride, M, (int)S, (T*)param, (T*)grad, K, ld, lr, ptr_vec);
@@ -1117,6 +1196,10 @@ extern "C" GA_API int ga_demo_encode(int dtype, const ga_demo_tensor* tensors, i
             launch_encode<__hip_bfloat16>(tensors, ntensors, nchunks, F, param, grad, delta, K, ld, lr, decay,
                                           wd_factor, payload, payload_stride, M, ptr_vec, stream);
             break;
+        case GA_BF16_REF:
+            launch_encode<__hip_bfloat16, true>(tensors, ntensors, nchunks, F, param, grad, delta, K, ld, lr, decay,
+                                                wd_factor, payload, payload_stride, M, ptr_vec, stream);
+            break;
         default: set_error("ga_demo_encode: unknown dtype %d", dtype); return GA_EINVAL;
     }
     return check_launch("ga_demo_encode");
@@ -1152,6 +1235,14 @@ extern "C" GA_API int ga_demo_decode(int dtype, const ga_demo_tensor* tensors, i
             else
                 launch_decode<__hip_bfloat16, uint16_t>(tensors, ntensors, nchunks, B, payload, payload_stride, M,
                                                         S, param, grad, K, ld, lr, ptr_vec, stream);
+            break;
+        case GA_BF16_REF:
+            if (S <= 255)
+                launch_decode<__hip_bfloat16, uint8_t, true>(tensors, ntensors, nchunks, B, payload, payload_stride,
+                                                             M, S, param, grad, K, ld, lr, ptr_vec, stream);
+            else
+                launch_decode<__hip_bfloat16, uint16_t, true>(tensors, ntensors, nchunks, B, payload, payload_stride,
+                                                              M, S, param, grad, K, ld, lr, ptr_vec, stream);
             break;
         default: set_error("ga_demo_decode: unknown dtype %d", dtype); return GA_EINVAL;
     }

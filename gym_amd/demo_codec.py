@@ -71,11 +71,24 @@ def dct_table(n):
     return c * np.cos(math.pi * (2 * i + 1) * k / (2 * n))
 
 
+BF16_TRANSFORMS = ("fp32", "reference")
+
+
 class DemoPlan:
-    def __init__(self, layout, chunk=64, topk=32):
+    """bf16_transform (bf16 arenas only): "fp32" -- fp32 DCT bases and fp32
+    arithmetic on the bf16 values (the product's default, closer to the exact
+    transform); "reference" -- the reference's bf16 arithmetic: bases rounded
+    to bf16 (demo.py:235-236) and every transform stage rounded to bf16 in the
+    reference's contraction order (ga_demo_encode / ga_demo_decode with
+    GA_BF16_REF; the block kernels)."""
+
+    def __init__(self, layout, chunk=64, topk=32, bf16_transform="fp32"):
+        if bf16_transform not in BF16_TRANSFORMS:
+            raise ValueError(f"bf16_transform must be one of {BF16_TRANSFORMS}, got {bf16_transform!r}")
         self.layout = layout
         self.chunk = int(chunk)
         self.topk = int(topk)
+        self.bf16_reference = bf16_transform == "reference"
         sizes, descs = [], []
         basis_of = {}
         payload_off = 0
@@ -105,7 +118,8 @@ class DemoPlan:
         self.nchunks = chunk_start
         # every chunk 64x64 or 1x64 with k <= 64: the wave-per-chunk encode applies
         # (ga_demo_encode_sym: the 64x64 tensors re-numbered, the 1x64 chunks in row groups)
-        self.wave_encode = all(d.n2 == TILE and d.n1 in (1, TILE) and d.k <= 64 for d in descs)
+        self.wave_encode = (not self.bf16_reference
+                            and all(d.n2 == TILE and d.n1 in (1, TILE) and d.k <= 64 for d in descs))
         self._wave_host = None
         if self.wave_encode:
             d64, groups, start = [], [], 0
@@ -133,8 +147,10 @@ class DemoPlan:
         for j, n in enumerate(sizes):
             F[j, :n, :n] = dct_table(n)
         self._F_host = torch.from_numpy(F.astype(np.float32))
+        if self.bf16_reference:  # the reference's bases cast to the parameter dtype (demo.py:235-236)
+            self._F_host = self._F_host.to(torch.bfloat16).to(torch.float32)
         # the inverse of an orthonormal basis is its transpose (idct(eye(n)), demo.py:398-442)
-        self._B_host = torch.from_numpy(np.ascontiguousarray(F.transpose(0, 2, 1)).astype(np.float32))
+        self._B_host = self._F_host.transpose(1, 2).contiguous()
         self.basis_sizes = sizes
         self._F64_host = self._F_host[basis_of[TILE]].contiguous() if TILE in basis_of else None
         self.device = None

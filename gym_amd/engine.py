@@ -419,10 +419,10 @@ class DeMoCodec:
     all-gather of the packed payloads, decode + sign-SGD applied to every
     replica.  Payload per node: int32 idx[M] then fp32 val[M]."""
 
-    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32):
+    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32, bf16_transform="fp32"):
         self.coll, self.K_local = coll, int(K_local)
         self.K_total = coll.world * self.K_local
-        self.plan = DemoPlan(layout, chunk=chunk, topk=topk).to(device)
+        self.plan = DemoPlan(layout, chunk=chunk, topk=topk, bf16_transform=bf16_transform).to(device)
         M = self.plan.M
         self.payload = torch.zeros(self.K_local, 2 * M, dtype=torch.int32, device=device)
         self.gathered = (torch.zeros(self.K_total, 2 * M, dtype=torch.int32, device=device)
@@ -509,13 +509,14 @@ def place_demo_step(encode, decode, P, G, D):
     return (bp, bg, bd), (p2, g2, d2), rec
 
 
-def demo_codec(coll: Collective, K_local, layout, device, chunk=64, topk=32):
+def demo_codec(coll: Collective, K_local, layout, device, chunk=64, topk=32, bf16_transform="fp32"):
     """The DeMo codec an exchange should use: pipelined over DEMO_PIECES tensor
     groups when the all-gather is an async RCCL collective across processes,
     else one encode -> all-gather -> decode."""
     if coll.rccl and coll.exchange and DEMO_PIECES > 1 and len(layout.numels) > 1:
-        return PipelinedDeMoCodec(coll, K_local, layout, device, chunk=chunk, topk=topk, pieces=DEMO_PIECES)
-    return DeMoCodec(coll, K_local, layout, device, chunk=chunk, topk=topk)
+        return PipelinedDeMoCodec(coll, K_local, layout, device, chunk=chunk, topk=topk, pieces=DEMO_PIECES,
+                                  bf16_transform=bf16_transform)
+    return DeMoCodec(coll, K_local, layout, device, chunk=chunk, topk=topk, bf16_transform=bf16_transform)
 
 
 def split_tensors(numels, pieces):
@@ -544,14 +545,16 @@ class PipelinedDeMoCodec:
     order are the ones of the unpipelined codec, so results are identical.
     Same call signature as DeMoCodec.__call__ (no custom all_gather)."""
 
-    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32, pieces=None):
+    def __init__(self, coll: Collective, K_local, layout, device, chunk=64, topk=32, pieces=None,
+                 bf16_transform="fp32"):
         self.coll = coll
         pieces = DEMO_PIECES if pieces is None else pieces
         groups = split_tensors(layout.numels, max(1, int(pieces)))
-        self.codecs = [DeMoCodec(coll, K_local, layout.subset(g), device, chunk=chunk, topk=topk) for g in groups]
+        self.codecs = [DeMoCodec(coll, K_local, layout.subset(g), device, chunk=chunk, topk=topk,
+                                 bf16_transform=bf16_transform) for g in groups]
         # every piece runs the kernel family the whole plan would (the wave-per-chunk
         # kernels only if every chunk of the model qualifies), so the results match
-        if not DemoPlan(layout, chunk=chunk, topk=topk).wave_encode:
+        if not DemoPlan(layout, chunk=chunk, topk=topk, bf16_transform=bf16_transform).wave_encode:
             for c in self.codecs:
                 c.plan.wave_encode = False
         self.M = sum(c.plan.M for c in self.codecs)

@@ -300,6 +300,16 @@ def sparta_scatter(vals, idx, count, cap, divisor, dst, layout="rows"):
                                   _p(dst2), K, ld, code, _stream()), "ga_sparta_scatter")
 
 
+def _demo_dtype(plan, t):
+    """The arena dtype code, or GA_BF16_REF for a bf16 arena under a plan with
+    the reference's bf16 arithmetic (DemoPlan(bf16_transform="reference"))."""
+    if getattr(plan, "bf16_reference", False):
+        if t.dtype != torch.bfloat16:
+            raise ValueError("DeMo bf16_transform='reference' applies to bf16 arenas only")
+        return _lib.GA_BF16_REF
+    return _dtype_code(t)
+
+
 def demo_encode(plan, param, grad, delta, payload, lr, decay, wd_factor):
     """plan: gym_amd.demo_codec.DemoPlan.  param/grad/delta: [K, ld] replica sets
     (or 1-D); payload: int32 [K, 2*M]."""
@@ -320,7 +330,7 @@ def demo_encode(plan, param, grad, delta, payload, lr, decay, wd_factor):
                                        float(lr), float(decay), float(wd_factor), _p(pl2), pl2.stride(0), plan.M,
                                        _stream()), "ga_demo_encode_sym")
         return
-    check(lib().ga_demo_encode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.F), _p(plan.B),
+    check(lib().ga_demo_encode(_demo_dtype(plan, p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.F), _p(plan.B),
                                _p(p2), _p(g2), _p(d2), K, ld, float(lr), float(decay), float(wd_factor), _p(pl2),
                                pl2.stride(0), plan.M, _stream()), "ga_demo_encode")
 
@@ -351,7 +361,7 @@ def demo_decode(plan, gathered, param, grad, lr):
                                        _p(plan.groups), plan.ngroups, _p(plan.F64), _p(ga), ga.stride(0), plan.M, S,
                                        _p(p2), _p(g2), K, ld, float(lr), _stream()), "ga_demo_decode_sym")
         return
-    check(lib().ga_demo_decode(_dtype_code(p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.B), _p(ga),
+    check(lib().ga_demo_decode(_demo_dtype(plan, p2), _p(plan.desc), plan.ntensors, plan.nchunks, _p(plan.B), _p(ga),
                                ga.stride(0), plan.M, S, _p(p2), _p(g2), K, ld, float(lr), _stream()),
           "ga_demo_decode")
 

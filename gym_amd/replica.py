@@ -112,7 +112,9 @@ class ReplicaRunner:
             # the codec covers the trainable tensors only, as DeMo's param list (demo.py:99-117)
             live = [i for i, p in enumerate(self.ra.arenas[0].params) if p.requires_grad]
             self.codec = demo_codec(self.coll, self.K, self.ra.layout.subset(live), dev,
-                                    chunk=kw["compression_chunk"], topk=kw["compression_topk"])
+                                    chunk=kw["compression_chunk"], topk=kw["compression_topk"],
+                                    bf16_transform=kw.get("bf16_transform", "fp32") if dt == torch.bfloat16
+                                    else "fp32")
         else:
             spec = s.optim_spec if isinstance(s, SimpleReduceStrategy) else s.inner_optim_spec
             if fusable(spec.cls, spec.kwargs, self.ra):

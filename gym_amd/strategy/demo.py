@@ -31,8 +31,9 @@ class DeMoStrategy(Strategy):
             "custom_all_gather": all_gather,
             "lr": self.kwargs.get("lr", 0.001),
         }
-        if "placement" in self.kwargs:  # gym_amd option: keep the arenas where they are
-            kw["placement"] = self.kwargs["placement"]
+        for opt in ("placement", "bf16_transform"):  # gym_amd options of the DeMo optimizer
+            if opt in self.kwargs:
+                kw[opt] = self.kwargs[opt]
         if hasattr(self, "strategy_config") and hasattr(self.strategy_config, "optimizer_kwargs"):
             kw.update(self.strategy_config.optimizer_kwargs)
         return kw

@@ -36,7 +36,7 @@ class DeMo(torch.optim.SGD):
     def __init__(self, params, compression_decay: float = 0.999, compression_topk: int = 32,
                  compression_chunk: int = 64, weight_decay: float = 0.0,
                  process_group: Optional[dist.ProcessGroup] = None, custom_all_gather=None, placement: bool = True,
-                 **kwargs):
+                 bf16_transform: str = "fp32", **kwargs):
         super().__init__(params, foreach=False, momentum=0.0, dampening=0.0, nesterov=False, maximize=False,
                          weight_decay=0.0, **kwargs)
         if compression_topk <= 0:
@@ -69,7 +69,13 @@ class DeMo(torch.optim.SGD):
         self.delta_flat = torch.zeros_like(self.arena.flat)
         # pipelined over tensor groups when the all-gather is async RCCL (engine.demo_codec);
         # a user-supplied custom_all_gather gets the one-exchange codec
-        self._codec_kw = dict(chunk=compression_chunk, topk=compression_topk)
+        # bf16 parameters: "fp32" bases and arithmetic (default) or the reference's own bf16
+        # transform ("reference": bf16 bases, every einsum stage rounded, demo.py:235-252)
+        if bf16_transform not in ("fp32", "reference"):
+            raise ValueError(f"bf16_transform must be 'fp32' or 'reference', got {bf16_transform!r}")
+        self.bf16_transform = bf16_transform
+        self._codec_kw = dict(chunk=compression_chunk, topk=compression_topk,
+                              bf16_transform=bf16_transform if self.default_dtype == torch.bfloat16 else "fp32")
         self.codec = (demo_codec(self.coll, 1, self.arena.layout, self.arena.device, **self._codec_kw)
                       if self._gather_fn() is None else
                       DeMoCodec(self.coll, 1, self.arena.layout, self.arena.device, **self._codec_kw))

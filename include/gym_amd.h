@@ -41,6 +41,13 @@ extern "C" {
 /* element types of arena buffers */
 #define GA_F32 0
 #define GA_BF16 1
+/* DeMo only (ga_demo_encode / ga_demo_decode): bf16 arenas with the reference's
+ * bf16 arithmetic -- bf16 DCT bases (the caller's F / B tables hold
+ * bf16-representable values), every stage of each transform rounded to bf16 in
+ * the reference's contraction order (chunk rows first), the delta rounded after
+ * the decay and after the gradient add (exogym/strategy/demo_impl/demo.py:
+ * 159-180, 235-252 as torch runs it). */
+#define GA_BF16_REF 2
 
 /* replica-set layouts (SPARTA entry points):
  *   GA_LAYOUT_ROWS        [K, ld]: replica k of element i at k*ld + i (every other kernel's layout)

@@ -591,6 +591,91 @@ def test_demo_bf16_vs_reference_bf16_golden(golden):
     agree.done()
 
 
+def _bf16_golden_step(z, step, L, plan, alpha):
+    """One G4b step through the codec kernels from the step's recorded state:
+    (P, G = sign, D per node) of replica 0 / every node, as bf16 tensors."""
+    from gym_amd import ops
+    K, ns = int(z["K"]), int(z["nshapes"])
+    lr, wd, decay = float(z["lr"]), float(z["wd"]), float(z["decay"])
+    P, D, G = (torch.zeros(K, L.n, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+    for i in range(ns):
+        for k in range(K):
+            L.views(P[k])[i].copy_(t(z[f"p_before_{step}_{i}"], torch.bfloat16))
+            L.views(D[k])[i].copy_(t(z[f"delta_before_{step}_{i}"][k], torch.bfloat16))
+            L.views(G[k])[i].copy_(t(z[f"grad_{step}_{i}"][k], torch.bfloat16))
+    payload = torch.zeros(K, 2 * plan.M, dtype=torch.int32, device=DEV)
+    P0 = P.clone()
+    ops.demo_encode(plan, P, G, D, payload, alpha, decay, float(np.float32(1.0 - lr * wd)))
+    ops.demo_decode(plan, payload, P, G, alpha)
+    return P0, P, G, D
+
+
+def test_demo_bf16_reference_transform_vs_golden(golden):
+    """DeMo(bf16_transform="reference") -- GA_BF16_REF: bf16 bases, every einsum
+    stage rounded to bf16 in the reference's contraction order, the delta rounded
+    after the decay and the add -- against G4b, with alpha rounded to bf16 as
+    torch's CPU add_ does.  The reference's CPU topk breaks the bf16 ties in its
+    own order (lowest index here), so the bar stays statistical
+    (demo_checks.Bf16Agreement, the same as the fp32-basis path's); the update is
+    torch's own bf16 ops on this GPU."""
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    z = golden("demo_steps_bf16.npz")
+    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
+    lr, wd = float(z["lr"]), float(z["wd"])
+    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
+    L = ArenaLayout(shapes)
+    plan = DemoPlan(L, chunk=int(z["chunk"]), topk=int(z["topk"]), bf16_transform="reference")
+    assert not plan.wave_encode
+    alpha = float(torch.tensor(lr).bfloat16().float())  # torch's CPU add_ rounds alpha to bf16
+    agree = demo_checks.Bf16Agreement()
+    for step in range(steps):
+        P0, P, G, D = _bf16_golden_step(z, step, L, plan, alpha)
+        want = P0.mul_(1.0 - lr * wd).add_(G, alpha=-alpha)
+        assert torch.equal(want, P), "bf16 p update differs from torch's bf16 mul_/add_ on the GPU"
+        for i in range(ns):
+            agree.check(host(L.views(G[0])[i]), host(L.views(P[0])[i]), [host(L.views(D[k])[i]) for k in range(K)],
+                        z, step, i)
+    agree.done()
+
+
+def test_demo_bf16_reference_transform_vs_torch_on_gpu(golden):
+    """GA_BF16_REF against the reference's op sequence as torch runs it on this
+    GPU (oracle/demo_bf16.py with device cuda: bf16 einsums on the GPU's GEMMs,
+    the GPU topk, fp32 alpha), from G4b's recorded states.  What can differ: the
+    fp32 accumulation order inside each GEMM before its bf16 rounding (a rare
+    last-bit flip of an intermediate) and ties among equal bf16 magnitudes."""
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    from oracle import demo_bf16 as ob
+    z = golden("demo_steps_bf16.npz")
+    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
+    lr, wd, decay = float(z["lr"]), float(z["wd"]), float(z["decay"])
+    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
+    L = ArenaLayout(shapes)
+    plan = DemoPlan(L, chunk=int(z["chunk"]), topk=int(z["topk"]), bf16_transform="reference")
+    sa, pe, de, n = [], 0, 0, 0
+    for step in range(steps):
+        _, P, G, D = _bf16_golden_step(z, step, L, plan, lr)
+        for i in range(ns):
+            rp, rd, rs = ob.demo_step(z[f"p_before_{step}_{i}"], list(z[f"delta_before_{step}_{i}"]),
+                                      list(z[f"grad_{step}_{i}"]), lr, decay, int(z["topk"]), int(z["chunk"]), wd,
+                                      device=DEV)
+            s = host(L.views(G[0])[i])
+            sa.append(float((s == rs).mean()))
+            pe += int((host(L.views(P[0])[i]) == rp).sum())
+            de += sum(int((host(L.views(D[k])[i]) == rd[k]).sum()) for k in range(K))
+            n += rp.size
+    assert min(sa) >= BF16_REF_SIGN_MIN and float(np.mean(sa)) >= BF16_REF_SIGN_ALL, sa
+    assert pe / n >= BF16_REF_SIGN_ALL and de / (K * n) >= BF16_REF_DELTA_EXACT, (pe / n, de / (K * n))
+
+
+# bars of the GA_BF16_REF path against torch's own bf16 ops on the GPU (measured r05d)
+BF16_REF_SIGN_MIN = 0.97
+BF16_REF_SIGN_ALL = 0.99
+BF16_REF_DELTA_EXACT = 0.97
+
+
 @pytest.mark.parametrize("kernel", ["wave", "block"])
 def test_demo_all_zero_chunk_tie_rule(monkeypatch, kernel):
     from gym_amd import ops

@@ -292,3 +292,24 @@ def test_lambda_cosine_matches_reference(golden):
         ref = z[name]
         got = [0.5 * osched.lambda_cosine(s, max_steps, **kw) for s in range(len(ref))]
         close(got, ref, rtol=1e-12, atol=1e-15)
+
+
+def test_bf16_reference_arithmetic_restatement_is_the_golden(golden):
+    """oracle/demo_bf16.py -- the reference's bf16 op sequence (bf16 bases,
+    two-stage einsums rounded per stage, the delta rounded after the decay and
+    after the add, torch.topk's CPU tie order, bf16 alpha) run with torch on
+    the CPU -- reproduces G4b bit for bit: parameters, signs and both nodes'
+    deltas after each of the three steps.  It pins the GA_BF16_REF kernels'
+    target arithmetic (tests/test_gpu_kernels.py)."""
+    from oracle import demo_bf16 as ob
+    z = golden("demo_steps_bf16.npz")
+    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
+    lr, wd, decay = float(z["lr"]), float(z["wd"]), float(z["decay"])
+    for step in range(steps):
+        for i in range(ns):
+            p, ds, s = ob.demo_step(z[f"p_before_{step}_{i}"], list(z[f"delta_before_{step}_{i}"]),
+                                    list(z[f"grad_{step}_{i}"]), lr, decay, int(z["topk"]), int(z["chunk"]), wd)
+            assert np.array_equal(s, z[f"sign_{step}_{i}"]), (step, i)
+            assert np.array_equal(p, z[f"p_after_{step}_{i}"]), (step, i)
+            for k in range(K):
+                assert np.array_equal(ds[k], z[f"delta_after_{step}_{i}"][k]), (step, i, k)
