@@ -610,41 +610,13 @@ def _bf16_golden_step(z, step, L, plan, alpha):
     return P0, P, G, D
 
 
-def test_demo_bf16_reference_transform_vs_golden(golden):
+def test_demo_bf16_reference_transform_is_torch_on_gpu(golden):
     """DeMo(bf16_transform="reference") -- GA_BF16_REF: bf16 bases, every einsum
     stage rounded to bf16 in the reference's contraction order, the delta rounded
-    after the decay and the add -- against G4b, with alpha rounded to bf16 as
-    torch's CPU add_ does.  The reference's CPU topk breaks the bf16 ties in its
-    own order (lowest index here), so the bar stays statistical
-    (demo_checks.Bf16Agreement, the same as the fp32-basis path's); the update is
-    torch's own bf16 ops on this GPU."""
-    from gym_amd.arena import ArenaLayout
-    from gym_amd.demo_codec import DemoPlan
-    z = golden("demo_steps_bf16.npz")
-    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
-    lr, wd = float(z["lr"]), float(z["wd"])
-    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
-    L = ArenaLayout(shapes)
-    plan = DemoPlan(L, chunk=int(z["chunk"]), topk=int(z["topk"]), bf16_transform="reference")
-    assert not plan.wave_encode
-    alpha = float(torch.tensor(lr).bfloat16().float())  # torch's CPU add_ rounds alpha to bf16
-    agree = demo_checks.Bf16Agreement()
-    for step in range(steps):
-        P0, P, G, D = _bf16_golden_step(z, step, L, plan, alpha)
-        want = P0.mul_(1.0 - lr * wd).add_(G, alpha=-alpha)
-        assert torch.equal(want, P), "bf16 p update differs from torch's bf16 mul_/add_ on the GPU"
-        for i in range(ns):
-            agree.check(host(L.views(G[0])[i]), host(L.views(P[0])[i]), [host(L.views(D[k])[i]) for k in range(K)],
-                        z, step, i)
-    agree.done()
-
-
-def test_demo_bf16_reference_transform_vs_torch_on_gpu(golden):
-    """GA_BF16_REF against the reference's op sequence as torch runs it on this
-    GPU (oracle/demo_bf16.py with device cuda: bf16 einsums on the GPU's GEMMs,
-    the GPU topk, fp32 alpha), from G4b's recorded states.  What can differ: the
-    fp32 accumulation order inside each GEMM before its bf16 rounding (a rare
-    last-bit flip of an intermediate) and ties among equal bf16 magnitudes."""
+    after the decay and after the add -- against the reference's op sequence as
+    torch runs it on this GPU (oracle/demo_bf16.py with device cuda: bf16 einsums
+    on the GPU's GEMMs, torch.topk on the GPU, fp32 alpha), from each of G4b's
+    recorded states: parameters, signs and both nodes' deltas BIT-IDENTICAL."""
     from gym_amd.arena import ArenaLayout
     from gym_amd.demo_codec import DemoPlan
     from oracle import demo_bf16 as ob
@@ -654,26 +626,49 @@ def test_demo_bf16_reference_transform_vs_torch_on_gpu(golden):
     shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
     L = ArenaLayout(shapes)
     plan = DemoPlan(L, chunk=int(z["chunk"]), topk=int(z["topk"]), bf16_transform="reference")
-    sa, pe, de, n = [], 0, 0, 0
+    assert not plan.wave_encode
     for step in range(steps):
-        _, P, G, D = _bf16_golden_step(z, step, L, plan, lr)
+        P0, P, G, D = _bf16_golden_step(z, step, L, plan, lr)
+        # the update is torch's own bf16 ops on this GPU, fed the kernel's signs
+        assert torch.equal(P0.mul_(1.0 - lr * wd).add_(G, alpha=-lr), P)
         for i in range(ns):
             rp, rd, rs = ob.demo_step(z[f"p_before_{step}_{i}"], list(z[f"delta_before_{step}_{i}"]),
                                       list(z[f"grad_{step}_{i}"]), lr, decay, int(z["topk"]), int(z["chunk"]), wd,
                                       device=DEV)
-            s = host(L.views(G[0])[i])
-            sa.append(float((s == rs).mean()))
-            pe += int((host(L.views(P[0])[i]) == rp).sum())
-            de += sum(int((host(L.views(D[k])[i]) == rd[k]).sum()) for k in range(K))
-            n += rp.size
-    assert min(sa) >= BF16_REF_SIGN_MIN and float(np.mean(sa)) >= BF16_REF_SIGN_ALL, sa
-    assert pe / n >= BF16_REF_SIGN_ALL and de / (K * n) >= BF16_REF_DELTA_EXACT, (pe / n, de / (K * n))
+            assert np.array_equal(host(L.views(G[0])[i]), rs), (step, i)
+            assert np.array_equal(host(L.views(P[0])[i]), rp), (step, i)
+            for k in range(K):
+                assert np.array_equal(host(L.views(D[k])[i]), rd[k]), (step, i, k)
 
 
-# bars of the GA_BF16_REF path against torch's own bf16 ops on the GPU (measured r05d)
-BF16_REF_SIGN_MIN = 0.97
-BF16_REF_SIGN_ALL = 0.99
-BF16_REF_DELTA_EXACT = 0.97
+def test_demo_bf16_reference_transform_vs_cpu_golden(golden):
+    """The same path against G4b itself (the reference's bf16 run on the CPU),
+    alpha rounded to bf16 as torch's CPU add_ does.  What still differs is the
+    CPU topk's order among tied bf16 magnitudes -- the reference run on the GPU
+    differs from its own CPU run by the same amount (tools/bf16_agreement.py:
+    sign agreement 0.939 worst tensor / 0.977 overall) -- so the bar is
+    demo_checks.Bf16Agreement's for signs and p, and the deltas bit-identical in
+    >= 60% of elements (the ones outside tie-affected chunks)."""
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    z = golden("demo_steps_bf16.npz")
+    K, steps, ns = int(z["K"]), int(z["steps"]), int(z["nshapes"])
+    lr, wd = float(z["lr"]), float(z["wd"])
+    shapes = [z[f"p_before_0_{i}"].shape for i in range(ns)]
+    L = ArenaLayout(shapes)
+    plan = DemoPlan(L, chunk=int(z["chunk"]), topk=int(z["topk"]), bf16_transform="reference")
+    alpha = float(torch.tensor(lr).bfloat16().float())
+    agree = demo_checks.Bf16Agreement(delta_rel=float("inf"))
+    same = total = 0
+    for step in range(steps):
+        _, P, G, D = _bf16_golden_step(z, step, L, plan, alpha)
+        for i in range(ns):
+            ds = [host(L.views(D[k])[i]) for k in range(K)]
+            agree.check(host(L.views(G[0])[i]), host(L.views(P[0])[i]), ds, z, step, i)
+            same += sum(int((d == z[f"delta_after_{step}_{i}"][k]).sum()) for k, d in enumerate(ds))
+            total += sum(d.size for d in ds)
+    agree.done()
+    assert same / total >= 0.6, same / total
 
 
 @pytest.mark.parametrize("kernel", ["wave", "block"])
@@ -1260,3 +1255,23 @@ def test_empty_inputs_every_kernel():
     torch.cuda.synchronize()
     assert (host(reps) == 5.0).all() and (host(master) == 2.0).all() and (host(vals) == 9.0).all()
     assert (host(idx) == -1).all()
+
+
+def test_demo_optimizer_bf16_transform_option():
+    """DeMo(bf16_transform=...) on bf16 parameters picks the plan (reference:
+    the GA_BF16_REF block kernels) and steps; fp32 parameters ignore it;
+    a bad value is rejected."""
+    from gym_amd.strategy.demo_impl.demo import DeMo
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(128, 64), torch.nn.Linear(64, 32)).to(DEV).to(torch.bfloat16)
+    opt = DeMo(m.parameters(), lr=1e-3, compression_topk=8, bf16_transform="reference", placement=False)
+    assert opt.codec.plan.bf16_reference and not opt.codec.plan.wave_encode
+    for _ in range(2):
+        opt.zero_grad()
+        m(torch.randn(16, 128, device=DEV, dtype=torch.bfloat16)).float().square().mean().backward()
+        opt.step()
+    assert all(torch.isfinite(p.float()).all() for p in m.parameters())
+    f = torch.nn.Linear(64, 64).to(DEV)
+    assert not DeMo(f.parameters(), bf16_transform="reference").codec.plan.bf16_reference
+    with pytest.raises(ValueError):
+        DeMo(f.parameters(), bf16_transform="bf8")

@@ -6,10 +6,6 @@ set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/r05d
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/dbg_placed_alias3.py > $O/va_overlap.txt 2>&1 || { echo "VA CHECK FAILED"; tail -20 $O/va_overlap.txt; exit 1; }
-tail -8 $O/va_overlap.txt
-timeout -k 10 300 python tools/bf16_agreement.py > $O/bf16_agreement.json 2> $O/bf16_agreement.err || { echo "BF16 AGREEMENT FAILED"; tail -20 $O/bf16_agreement.err; exit 1; }
-cat $O/bf16_agreement.json
 timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -k "demo" -x -q --timeout 240 --timeout-method thread > $O/demo_tests.log 2>&1 || { echo "DEMO TESTS FAILED"; tail -30 $O/demo_tests.log; exit 1; }
 tail -2 $O/demo_tests.log
 GA_BENCH_BACKEND=gloo GA_BENCH_WATCHDOG=120 timeout -k 10 900 python bench.py --gpus 8 --steps 3 --warmup 1 > $O/bench_gloo8_selflaunch.json 2> $O/bench_gloo8_selflaunch.err || { echo "GLOO8 FAILED"; tail -40 $O/bench_gloo8_selflaunch.err; exit 1; }
