@@ -812,7 +812,8 @@ def bench_inner_adamw(args, coll, dev, model="gpt2-124m", max_norm=1.0):
             "torch_adamw_foreach_ms": round(tt * 1e3, 4), "speedup_vs_torch": round(tt / t, 2),
             "placement": {k: v for k, v in (opt.placement or {}).items() if k != "probe_ms"} or None,
             "placement_probe_ms_best_vs_ordinary": ([round(min(opt.placement["probe_ms"]), 4),
-                                                     opt.placement["probe_ms"][0]] if opt.placement else None)}
+                                                     opt.placement["probe_ms"][0]]
+                                                    if opt.placement and "probe_ms" in opt.placement else None)}
 
 
 def free_port():

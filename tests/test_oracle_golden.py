@@ -313,3 +313,28 @@ def test_bf16_reference_arithmetic_restatement_is_the_golden(golden):
             assert np.array_equal(p, z[f"p_after_{step}_{i}"]), (step, i)
             for k in range(K):
                 assert np.array_equal(ds[k], z[f"delta_after_{step}_{i}"][k]), (step, i, k)
+
+
+def test_demo_plan_bf16_reference_tables(golden):
+    """DemoPlan(bf16_transform="reference"): the DCT / inverse tables the
+    GA_BF16_REF kernels read are the reference's bases cast to bf16
+    (demo.py:235-236; the reference's own F/B from tests/golden/demo_codec.npz),
+    transposes of each other, and the wave kernels are off."""
+    import torch
+    from gym_amd.arena import ArenaLayout
+    from gym_amd.demo_codec import DemoPlan
+    z = golden("demo_codec.npz")
+    L = ArenaLayout([(128, 128), (64,), (96, 48)])
+    ref = DemoPlan(L, bf16_transform="reference")
+    plain = DemoPlan(L)
+    assert not ref.wave_encode and ref.bf16_reference and not plain.bf16_reference
+    F, B = ref._F_host, ref._B_host
+    assert torch.equal(B, F.transpose(1, 2))
+    assert torch.equal(F, plain._F_host.to(torch.bfloat16).float())
+    for j, n in enumerate(ref.basis_sizes):
+        key = f"F_{n}"
+        if key in z.files:  # the reference's FFT-built basis, cast as the reference casts it
+            want = torch.from_numpy(np.asarray(z[key], np.float32)).to(torch.bfloat16).float()
+            assert torch.equal(F[j, :n, :n], want), n
+    with pytest.raises(ValueError):
+        DemoPlan(L, bf16_transform="half")
