@@ -20,25 +20,13 @@ namespace ga {
 constexpr int kBlock = 256;
 constexpr int64_t kChunk = 1024;  // vectors (or scalars) per workgroup
 
-// The grid's share per workgroup, rounded up to whole passes of the block: kChunk
-// for the large arenas (chunk_grid launches ceil(total / kChunk) workgroups), finer
-// for small ones, so that they still spread over every CU (GPT-2 char-level, 3.7 MB:
-// 227 workgroups of 1024 vectors left 29 of the 256 CUs idle; 908 of 256 now).
-// Results do not depend on the split: every vector is summed on its own.
 __device__ __forceinline__ void chunk_range(int64_t total, int64_t& lo, int64_t& hi) {
-    const int64_t per = (total + gridDim.x - 1) / gridDim.x;
-    const int64_t chunk = (per + kBlock - 1) / kBlock * kBlock;
-    lo = (int64_t)blockIdx.x * chunk;
-    hi = lo + chunk < total ? lo + chunk : total;
+    lo = (int64_t)blockIdx.x * kChunk;
+    hi = lo + kChunk < total ? lo + kChunk : total;
 }
 
-constexpr int64_t kMinGrid = 2048;  // below this many kChunk workgroups, split finer (>= 1 pass each)
 inline int chunk_grid(int64_t total) {
-    int64_t g = ceil_div(total, kChunk);
-    if (g < kMinGrid) {
-        g = ceil_div(total, (int64_t)kBlock);
-        if (g > kMinGrid) g = kMinGrid;
-    }
+    const int64_t g = ceil_div(total, kChunk);
     return (int)(g < 1 ? 1 : g);
 }
 
