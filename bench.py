@@ -275,8 +275,9 @@ def xgmi_block(kind, nbytes, coll_ms, world, step_ms=None, what=None, latency_bo
     """The SURVEY §8(d) xGMI rooflines of one exchange at `world` GPUs.
     all_reduce of S bytes (or reduce-scatter + all-gather, the same bytes):
     bus bytes 2(G-1)/G * S; all_gather of a P-byte per-rank payload: (G-1) * P.
-    Fractions against one 153 GB/s link (the per-link ring model) and against
-    7 links; coll_ms = the collective timed alone, step_ms = the whole step."""
+    Fractions against one 153 GB/s link (the per-link ring model, SURVEY §8(d)'s
+    primary roofline), against the (G-1)-link multi-ring bound and against 7
+    links; coll_ms = the collective timed alone, step_ms = the whole step."""
     G = world
     bus = (2.0 * (G - 1) / G * nbytes) if kind == "all_reduce" else float((G - 1) * nbytes)
     out = {"collective": kind, "bytes": int(nbytes), "bus_bytes": int(bus), "world": G,
@@ -288,8 +289,11 @@ def xgmi_block(kind, nbytes, coll_ms, world, step_ms=None, what=None, latency_bo
         return out
     bw = bus / (coll_ms * 1e-3) / 1e9
     t_min = bus / (XGMI_LINK_GBS * 1e9) * 1e3
+    # the per-link ring model is the primary roofline; the multi-ring
+    # bound is (G - 1) links of a fully connected node (7 at G = 8)
     out.update({"bus_GBps": round(bw, 1), "t_min_per_link_ring_ms": round(t_min, 4),
                 "frac_per_link_ring": round(bw / XGMI_LINK_GBS, 4),
+                "frac_multi_ring": round(bw / ((G - 1) * XGMI_LINK_GBS), 4),
                 "frac_7link": round(bw / (7 * XGMI_LINK_GBS), 4)})
     if step_ms is not None:
         sbw = bus / (step_ms * 1e-3) / 1e9
