@@ -1,0 +1,16 @@
+#!/bin/bash
+# r05h: DeMo encode with its two DCT products on split bf16 MFMAs (in-tree library) vs
+# the f32-MFMA build (build/libgym_amd_base.so): DeMo kernel parity of the new build,
+# then interleaved timing of both builds in one process (tools/exp_demo_ablate.py).
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/r05h
+mkdir -p $O
+export TMPDIR=/tmp
+B=$GRAFT_REPO_ROOT/build/libgym_amd_base.so
+N=$GRAFT_REPO_ROOT/gym_amd/_lib/libgym_amd.so
+timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -k "demo" -x -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+timeout -k 10 300 python tools/exp_demo_ablate.py --codec 3 $B $N > $O/ab_encode.txt 2>&1 || { echo "AB FAILED"; tail -20 $O/ab_encode.txt; exit 1; }
+cat $O/ab_encode.txt
+timeout -k 10 300 python tools/exp_demo_ablate.py --codec 3 $N $B > $O/ab_encode2.txt 2>&1 || { echo "AB2 FAILED"; tail -20 $O/ab_encode2.txt; exit 1; }
+cat $O/ab_encode2.txt
