@@ -15,6 +15,9 @@ Process-group setup (the north star's "process-group setup in trainer.py"):
   - more nodes than GPUs (and a multiple of them): one process per GPU hosts
     num_nodes / GPUs simulated nodes on a [K, ld] replica arena
     (gym_amd.replica, replicas_per_process="auto"), RCCL across the GPUs;
+    their forward/backward passes run node by node (replica_forward="loop",
+    the default) or as one torch.func.vmap over the arena rows
+    (replica_forward="vmap", replica_vmap_chunk=nodes per vmap);
   - otherwise (or replicas_per_process=1) nodes share GPUs round-robin over a
     gloo group (RCCL cannot put two ranks on one GPU).
   - MASTER_ADDR is 127.0.0.1; device "cpu"/"mps" is refused (the step kernels

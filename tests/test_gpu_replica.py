@@ -66,3 +66,14 @@ def test_replica_eval_average_gpu():
     avg, rows = R.replica_eval_average(3, "cuda:0", False)
     assert not np.array_equal(rows[0], rows[1])
     assert np.array_equal(avg, mean_reduce(list(rows)))  # ascending in-kernel sum, true division: bit-exact
+
+
+@pytest.mark.parametrize("strategy", ["simple", "sparta", "diloco"])
+def test_replica_forward_vmap_matches_loop_gpu(strategy):
+    """replica_forward="vmap" (one torch.func.vmap over the arena rows, BatchNorm
+    and causal SDPA in the model) trains K = 3 nodes with the HIP kernels to the
+    per-node loop's parameters (fp32 rounding of the batched GEMMs only)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from test_replica_vmap import _train, assert_states_close
+    assert_states_close(_train("loop", "cuda:0", strategy), _train("vmap", "cuda:0", strategy))
