@@ -41,7 +41,8 @@ def test_diloco_outer_adam_replicas_bit_exact_gpu(tmp_path):
     R.compare(proc, rep, rtol=0, atol=0)
 
 
-def test_local_trainer_fit_replica_mode():
+@pytest.mark.parametrize("forward", ["loop", "vmap"])
+def test_local_trainer_fit_replica_mode(forward):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from tiny_models import TinyMLP, dataset
@@ -49,10 +50,10 @@ def test_local_trainer_fit_replica_mode():
     from gym_amd.trainer import LocalTrainer
     torch.manual_seed(0)
     model = TinyMLP()
-    tr = LocalTrainer(model, dataset(256), dataset(64, seed=1), start_port=22400)
+    tr = LocalTrainer(model, dataset(256), dataset(64, seed=1), start_port=22400 if forward == "loop" else 22410)
     final = tr.fit(num_epochs=1, strategy=SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-2)),
                    num_nodes=4, max_steps=6, devices=[0], batch_size=16, minibatch_size=8, val_size=16,
-                   val_interval=3, replicas_per_process=4)
+                   val_interval=3, replicas_per_process=4, replica_forward=forward, replica_vmap_chunk=2)
     assert final is not None
     for p in final.parameters():
         assert torch.isfinite(p).all()
