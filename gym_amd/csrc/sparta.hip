@@ -62,6 +62,48 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
     return c;
 }
 
+// torch's stream calls Philox with counter {ctr, t}: the 16 calls t = t0 .. t0 + 15 of
+// one 64-element word (t0 % 16 == 0) share ctr and t >> 32, so round 1's ctr product
+// and round 2's second product are the same for all of them: computed once per word
+// (TorchCtr), each call then issues 18 products instead of 20 (bit-identical words)
+struct TorchCtr {
+    uint32_t A, B, C, D;  // ctr_hi ^ k0.x; hi(P) ^ k1.x; lo(P); lo(M0 ctr_lo) ^ k1.y (P: round 2's second product)
+};
+
+__device__ __forceinline__ TorchCtr torch_ctr(uint2 k, uint64_t ctr, uint32_t t_hi) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+    const uint64_t p0 = mul_wide(M0, (uint32_t)ctr);                           // round 1: M0 * c.x
+    const uint32_t z1 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), t_hi, k.y, 0x96);  // round 1's c.z
+    const uint64_t p1 = mul_wide(M1, z1);                                      // round 2: M1 * c.z
+    TorchCtr T;
+    T.A = (uint32_t)(ctr >> 32) ^ k.x;
+    T.B = (uint32_t)(p1 >> 32) ^ (k.x + W0);
+    T.C = (uint32_t)p1;
+    T.D = (uint32_t)p0 ^ (k.y + W1);
+    return T;
+}
+
+// philox4x32_10({ctr, t}, k) for t_lo = (uint32_t)t, given torch_ctr(k, ctr, t >> 32)
+__device__ __forceinline__ uint4 torch_philox(const TorchCtr& T, uint32_t t_lo, uint2 k) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+    const uint64_t a = mul_wide(M1, t_lo);                                     // round 1: M1 * c.z
+    const uint64_t b = mul_wide(M0, (uint32_t)(a >> 32) ^ T.A);                 // round 2: M0 * c.x
+    uint4 c = make_uint4((uint32_t)a ^ T.B, T.C, (uint32_t)(b >> 32) ^ T.D, (uint32_t)b);
+    k.x += 2u * W0;
+    k.y += 2u * W1;
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+        const uint64_t p0 = mul_wide(M0, c.x), p1 = mul_wide(M1, c.z);
+        c = make_uint4(__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k.x, 0x96), (uint32_t)p1,
+                       __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k.y, 0x96), (uint32_t)p0);
+        k.x += W0;
+        k.y += W1;
+    }
+    return c;
+}
+
 struct Pred {
     const uint8_t* mask;  // uint8 mask arena, or null
     const uint64_t* bits; // packed mask (bit j of word w = element 64 w + j), or null; both null -> Philox
@@ -122,15 +164,12 @@ __device__ __forceinline__ uint64_t torch_word(uint2 key, uint64_t ctr, uint64_t
     // element against three for compare + select + or (torch_draw 0.069 ->
     // 0.067 ms, profiles/r02z_ab_torch_asmpack.txt)
     const uint32_t vthr = thr;
+    const TorchCtr T = torch_ctr(key, ctr, (uint32_t)(t0 >> 32));
 #pragma unroll
     for (int c0 = 12; c0 >= 0; c0 -= 4) {
         uint4 w[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint64_t t = t0 + c0 + c;
-            w[c] = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
-                                 key);
-        }
+        for (int c = 0; c < 4; ++c) w[c] = torch_philox(T, (uint32_t)t0 + (uint32_t)(c0 + c), key);
         uint32_t& acc = half[c0 >> 3];
 #pragma unroll
         for (int c = 3; c >= 0; --c) {
@@ -1142,15 +1181,13 @@ __global__ __launch_bounds__(kTbWordLanes) void probe_philox_kernel(int64_t nwor
     const int64_t wd = (int64_t)blockIdx.x * kTbWordLanes + threadIdx.x;
     if (wd >= nwords) return;
     uint32_t acc = 0u;
+    const uint64_t t0 = (uint64_t)wd * 16;
+    const TorchCtr T = torch_ctr(key, ctr, (uint32_t)(t0 >> 32));
 #pragma unroll
     for (int c0 = 0; c0 < 16; c0 += 4) {
         uint4 w[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint64_t t = (uint64_t)wd * 16 + c0 + c;
-            w[c] = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32)),
-                                 key);
-        }
+        for (int c = 0; c < 4; ++c) w[c] = torch_philox(T, (uint32_t)t0 + (uint32_t)(c0 + c), key);
 #pragma unroll
         for (int c = 0; c < 4; ++c)
             acc = __builtin_amdgcn_bitop3_b32(acc, __builtin_amdgcn_bitop3_b32(w[c].x, w[c].y, w[c].z, 0x96), w[c].w,

@@ -116,6 +116,12 @@ def main():
             alg = 2 * 4 * K * int(round(layout.n * p))
         ms = timed(step, launches)
         out.update(model="gpt2-124m", K=K, p=p, tensors=len(layout.numels))
+    elif mode == "probe_philox":  # the reference draw's Philox issue ceiling (ga_probe_philox)
+        layout = ArenaLayout(MODELS["gpt2-124m"]())
+        sink = torch.zeros(4, dtype=torch.int32, device=dev)
+        ms = timed(lambda: ops.probe_philox(layout.n, sink), launches)
+        alg = 0
+        out.update(model="gpt2-124m")
     elif mode == "probe_rows":  # the random-word floor of the rows layout (ga_probe_random_words)
         layout = ArenaLayout(MODELS["gpt2-124m"]())
         K, p = 32, 0.005
