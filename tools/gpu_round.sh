@@ -27,4 +27,9 @@ if [ "${REHEARSE:-1}" != "0" ]; then
   GA_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 1 > $O/bench_gloo2_rehearsal.json 2> $O/bench_gloo2_rehearsal.err || { echo "GLOO2 REHEARSAL FAILED"; tail -20 $O/bench_gloo2_rehearsal.err; exit 1; }
   tail -c 400 $O/bench_gloo2_rehearsal.json
 fi
+# the driver's N > 1 form (torchrun around bench.py; rank 0 times the CPU baseline first; TORCHRUN=1)
+if [ "${TORCHRUN:-0}" = "1" ]; then
+  GA_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29614 bench.py --gpus 2 --steps 5 --warmup 1 > $O/bench_gloo2_torchrun.json 2> $O/bench_gloo2_torchrun.err || { echo "GLOO2 TORCHRUN REHEARSAL FAILED"; tail -20 $O/bench_gloo2_torchrun.err; exit 1; }
+  tail -c 300 $O/bench_gloo2_torchrun.json
+fi
 echo DONE
