@@ -400,7 +400,8 @@ class BatchedForward:
     attention without mask or dropout runs as ONE fused-kernel call over the
     nodes folded into its batch dim (_FoldedSDPA; the fused kernels' backward
     has no batching rule on this stack), with a mask or dropout on the math
-    backend.
+    backend.  BatchNorm under bf16 autocast does not batch (torch's vmap rule
+    for batch_norm rejects autocast's mixed dtypes): such models keep the loop.
 
     Measured on MI355X (tools/exp_replica_vmap.py, profiles/r05k_replica_vmap.txt),
     32 nodes: the reference's char-level nanoGPT preset (4 layers, d 128, 16 x

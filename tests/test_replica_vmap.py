@@ -19,12 +19,13 @@ class TinyNet(nn.Module):
     forward takes the (x, y) minibatch and returns the loss (TrainNode's
     contract, exogym/train_node.py:145-175)."""
 
-    def __init__(self, seed=3, masked=False):
+    def __init__(self, seed=3, masked=False, norm="bn"):
         super().__init__()
         self.masked = masked  # an explicit mask: the math-backend path of BatchedForward's attention
+        self.norm = norm
         torch.manual_seed(seed)
         self.lin = nn.Linear(8, 16, bias=False)  # BatchNorm follows: a bias would get ~0 gradients that AdamW amplifies
-        self.bn = nn.BatchNorm1d(16)
+        self.bn = nn.BatchNorm1d(16) if norm == "bn" else nn.LayerNorm(16)
         self.qkv = nn.Linear(16, 48, bias=False)  # (a key bias gets ~0 gradients too: softmax is shift-invariant)
         self.head = nn.Linear(16, 4)
 
@@ -32,7 +33,7 @@ class TinyNet(nn.Module):
         x, y = batch
         B, T, _ = x.shape
         h = self.lin(x)
-        h = self.bn(h.transpose(1, 2)).transpose(1, 2)
+        h = self.bn(h.transpose(1, 2)).transpose(1, 2) if self.norm == "bn" else self.bn(h)
         q, k, v = (t.reshape(B, T, 2, 8).transpose(1, 2) for t in self.qkv(h).split(16, dim=-1))
         if self.masked:
             mask = torch.ones(T, T, dtype=torch.bool, device=x.device).tril()
@@ -148,3 +149,40 @@ def test_replica_trainnode_vmap_matches_loop(fake):  # noqa: F811
 def test_replica_forward_rejects_unknown_mode(fake):  # noqa: F811
     with pytest.raises(ValueError):
         _train("graph")
+
+
+def test_batched_forward_under_autocast():
+    """bf16 autocast around the batched forward (ReplicaTrainNode(autocast=True)):
+    the folded attention's backward recomputes under the forward's autocast
+    state; gradients match the per-node loop under the same autocast.  (LayerNorm:
+    torch's vmap rule for batch_norm rejects autocast's mixed dtypes on this
+    stack, so BatchNorm models under autocast keep the loop.)"""
+    import contextlib
+
+    from gym_amd.arena import ReplicaArena
+    from gym_amd.replica import BatchedForward
+    K = 2
+    models = [TinyNet(norm="ln") for _ in range(K)]
+    ra = ReplicaArena(models)
+    data = _batches(K, 1, seed=3)
+    b0 = _bufs(models)
+
+    def ac():
+        return torch.autocast(device_type="cpu", dtype=torch.bfloat16)
+
+    ra.zero_grad()
+    for k, m in enumerate(models):
+        with ac():
+            loss = m(data[k][0])
+        loss.backward()
+    ra.sync_grads()
+    g_loop = ra.grad_set.clone()
+    with torch.no_grad():
+        for m, bs in zip(models, b0):
+            for b, v in zip(m.buffers(), bs):
+                b.copy_(v)
+    ra.zero_grad()
+    BatchedForward(models, ra)([data[k][0] for k in range(K)], ac)
+    ra.sync_grads()
+    assert ra.grad_set.abs().sum() > 0
+    np.testing.assert_allclose(ra.grad_set.numpy(), g_loop.numpy(), rtol=2e-2, atol=2e-3)
