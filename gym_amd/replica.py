@@ -336,12 +336,12 @@ class _FoldedSDPA(torch.autograd.Function):
     def backward(ctx, grad_out):
         q, k, v = ctx.saved_tensors
         dt, enabled, dtype = ctx.amp
+        want = ctx.needs_input_grad[:3]
         with torch.enable_grad(), torch.autocast(device_type=dt, dtype=dtype, enabled=enabled):
-            qq, kk, vv = (t.detach().requires_grad_(t.requires_grad) for t in (q, k, v))
+            qq, kk, vv = (t.detach().requires_grad_(w) for t, w in zip((q, k, v), want))
             out = _SDPA(qq, kk, vv, is_causal=ctx.is_causal, scale=ctx.scale)
-            need = [t for t in (qq, kk, vv) if t.requires_grad]
-            got = iter(torch.autograd.grad(out, need, grad_out))
-        return tuple(next(got) if t.requires_grad else None for t in (qq, kk, vv)) + (None, None)
+            got = iter(torch.autograd.grad(out, [t for t, w in zip((qq, kk, vv), want) if w], grad_out))
+        return tuple(next(got) if w else None for w in want) + (None, None)
 
     @staticmethod
     def vmap(info, in_dims, q, k, v, is_causal, scale):
@@ -379,7 +379,9 @@ def _vmappable_attention():
 
 
 def _stack(batches):
-    """K minibatches (tensors or tuples of tensors) -> one with a leading K dim."""
+    """K minibatches (tensors, or tuples / dicts of tensors) -> one with a leading K dim."""
+    if isinstance(batches[0], dict):
+        return {key: torch.stack([b[key] for b in batches]) for key in batches[0]}
     if isinstance(batches[0], (tuple, list)):
         return tuple(torch.stack(parts) for parts in zip(*batches))
     return torch.stack(batches)
