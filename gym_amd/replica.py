@@ -371,11 +371,12 @@ def _vmappable_attention():
     the batched forward runs (models that call it through the module, as
     nanoGPT and nn.MultiheadAttention do)."""
     F = torch.nn.functional
+    prev = F.scaled_dot_product_attention
     F.scaled_dot_product_attention = _sdpa_vmappable
     try:
         yield
     finally:
-        F.scaled_dot_product_attention = _SDPA
+        F.scaled_dot_product_attention = prev
 
 
 def _stack(batches):
@@ -425,7 +426,11 @@ class BatchedForward:
         if len(self.names) != len(ra.layout.shapes):
             raise ValueError("BatchedForward: the model's parameters do not match the arena layout")
         self.buf_names = [n for n, _ in m0.named_buffers()]
-        self.meta = copy.deepcopy(m0).to("meta")
+        # a storage-free copy of the module (functional_call supplies every tensor)
+        memo = {id(p): torch.nn.Parameter(torch.empty_like(p, device="meta"), requires_grad=p.requires_grad)
+                for p in m0.parameters()}
+        memo.update({id(b): torch.empty_like(b, device="meta") for b in m0.buffers()})
+        self.meta = copy.deepcopy(m0, memo)
 
         def loss_of(params, bufs, batch):
             return functional_call(self.meta, (dict(zip(self.names, params)), bufs), (batch,))
