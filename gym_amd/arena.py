@@ -81,6 +81,14 @@ class ReplicaSet:
     def replica(self, k):
         return self.data[k]
 
+    def relocate(self, data):
+        """Move the replicas into another [K, ld] buffer (contents copied)."""
+        if data.shape != self.data.shape or data.dtype != self.data.dtype:
+            raise ValueError("ReplicaSet.relocate: a buffer of the set's shape and dtype")
+        if data.data_ptr() != self.data.data_ptr():
+            data.copy_(self.data)
+        self.data = data
+
     def views(self, k):
         return self.layout.views(self.data[k])
 
@@ -168,16 +176,20 @@ class ParamArena:
         with torch.no_grad():
             if flat.data_ptr() != self.flat.data_ptr():
                 flat.copy_(self.flat)
-            self.flat = flat
-            for p, v in zip(self.params, self.layout.views(flat)):
-                p.data = v
-            self._data_ptrs = [p.data_ptr() for p in self.params]
+            self._bind(flat)
             if self.grad_flat is not None:
                 if grad_flat.data_ptr() != self.grad_flat.data_ptr():
                     grad_flat.copy_(self.grad_flat)
                 self.grad_flat = grad_flat
                 self._grad_views = self.layout.views(grad_flat)
                 self.rebind_grads()
+
+    def _bind(self, flat):
+        """Point every parameter's .data at its view of `flat` (contents already there)."""
+        self.flat = flat
+        for p, v in zip(self.params, self.layout.views(flat)):
+            p.data = v
+        self._data_ptrs = [p.data_ptr() for p in self.params]
 
     def rebind_grads(self):
         """Point every trainable parameter's .grad back at its arena view."""
@@ -221,6 +233,20 @@ class ReplicaArena:
     def sync_grads(self):
         for a in self.arenas:
             a.sync_grads()
+
+    def relocate_params(self, flat_set):
+        """Move the K parameter rows into another [K, ld] buffer (contents copied;
+        every model's parameters re-pointed at their views of the new rows;
+        gradients stay): how the DiLoCo outer step moves the replica set into
+        the memory its step runs fastest on (engine.DiLoCoOuter._place)."""
+        if flat_set.shape != self.flat_set.shape or flat_set.dtype != self.flat_set.dtype:
+            raise ValueError("ReplicaArena.relocate_params: a buffer of the parameter set's shape and dtype")
+        with torch.no_grad():
+            if flat_set.data_ptr() != self.flat_set.data_ptr():
+                flat_set.copy_(self.flat_set)
+            self.flat_set = flat_set
+            for k, a in enumerate(self.arenas):
+                a._bind(flat_set[k])
 
     def zero_grad(self):
         if self.grad_set is not None:

@@ -169,6 +169,9 @@ class MeanReduce:
 # before the first outer step; the fastest is kept
 PLACEMENT_CANDIDATES = 64
 PLACEMENT_MAX_FRAC = 0.3  # of the free device memory the candidates may take at once
+# fresh [K, ld] replica sets probed first when the caller lets the step move its replica
+# set (DiLoCoOuter.relocate_replicas: the replica loop's ReplicaArena, the bench's set)
+REPLICA_PLACEMENT_CANDIDATES = 12
 
 
 class DiLoCoOuter:
@@ -201,6 +204,10 @@ class DiLoCoOuter:
         self.placement = None  # the placement probe's record (bench / DESIGN)
         self._placed_for = None
         self._placed = None  # the candidate buffer holding the state, when one was chosen
+        # relocate_replicas(new): moves the caller's [K, ld] replica set into `new` (contents
+        # copied, the caller's views re-pointed); None: the replica set stays where it is
+        self.relocate_replicas = None
+        self._reps_placed = None
         self.first = True
         self.dtype = dtype
         self.sum = torch.empty(n, device=device, dtype=dtype) if (X and not self.shard) else None
@@ -240,21 +247,32 @@ class DiLoCoOuter:
         ga_probe_diloco_placement -- the step's exact access pattern, every value
         written back unchanged -- beside the ordinary allocation; the fastest
         keeps the state, the others are released.  ~0.2 s once; at most
-        PLACEMENT_MAX_FRAC of the free memory at a time."""
+        PLACEMENT_MAX_FRAC of the free memory at a time.
+
+        The replica set's own region matters as much (r04i: with the replica set in a
+        slow class no master placement reaches the fast one), so when the caller
+        can move it (relocate_replicas) up to REPLICA_PLACEMENT_CANDIDATES fresh
+        [K, ld] sets are probed first, against the ordinary master, and the replica
+        set moves to the fastest when it beats its own.  Returns the replica set
+        to use from now on."""
         key = (reps.data_ptr(), reps.stride(0))
         if self._placed_for == key:
-            return
+            return reps
         self._placed_for = key
         per = self.per
         from . import placement
         ok, why = placement.policy(self.place_opt)
         if not ok:
             self.placement = {"placed": False, "why": why}
-            return
+            return reps
         if (self.coll.exchange or reps.device.type != "cuda" or reps.dtype != torch.float32 or self.mom is None
                 or reps.shape[0] > 16 or 4 * per < SHARD_MIN_BYTES or PLACEMENT_CANDIDATES < 2
                 or reps.stride(1) != 1 or reps.stride(0) % 4 or per % 4):
-            return
+            return reps
+        rep_rec = None
+        if self.relocate_replicas is not None and REPLICA_PLACEMENT_CANDIDATES >= 2 and reps.is_contiguous():
+            reps, rep_rec = self._place_replicas(reps, per)
+            self._placed_for = (reps.data_ptr(), reps.stride(0))
         src = reps[:, :per]
 
         def probe_state(state):
@@ -273,12 +291,41 @@ class DiLoCoOuter:
         self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
                           "how": "master+momentum in fresh device allocations probed with the step's "
                                  "access pattern; candidate 0 = the ordinary allocation"}
+        if rep_rec is not None:
+            self.placement["replica_set"] = rep_rec
+        return reps
+
+    def _place_replicas(self, reps, per):
+        """Stage 1 of _place: fresh [K, ld] replica sets probed against the
+        current master/momentum; the caller's set moves to the fastest one when
+        it beats the set's own time (relocate_replicas copies the contents)."""
+        from . import placement
+        K, ld = reps.shape
+
+        def as_set(buf):
+            return buf.tensor()[:K * ld].view(K, ld)
+
+        def probe(t):
+            return placement.time_probe(lambda: ops.probe_diloco_placement(t[:, :per], per, self.master, self.mom))
+
+        best_buf, times = placement.choose(4 * K * ld, reps.device, lambda b: probe(as_set(b)), probe(reps),
+                                           REPLICA_PLACEMENT_CANDIDATES, PLACEMENT_MAX_FRAC)
+        best = 0
+        if best_buf is not None:
+            best = min(range(len(times)), key=lambda i: times[i])
+            new = as_set(best_buf)
+            self.relocate_replicas(new)
+            self._reps_placed = best_buf
+            reps = new
+        return reps, {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
+                      "how": "the caller's replica set moved to the fastest of fresh [K, ld] allocations "
+                             "(probed against the ordinary master); candidate 0 = where it was"}
 
     def __call__(self, reps):
         n = self.n
         self.launch_elems = []
         if not self.coll.exchange:  # one kernel: read every replica, update, write every replica
-            self._place(reps)
+            reps = self._place(reps)
             self._outer(reps[:, :n], self.K_total, reps[:, :n])
         elif not self.shard:  # gloo: all-reduce the sum, replicated update
             ops.replica_mean(reps, self.sum, n=n, divisor=1.0)

@@ -124,7 +124,7 @@ class ArenaAdam(torch.optim.Optimizer):
         if len(self.param_groups) != 1:
             raise ValueError("ArenaAdam: one parameter group (the node's arena)")
         self.arenas = list(getattr(arena, "arenas", [arena]))
-        self.P = arena.flat_set if hasattr(arena, "flat_set") else arena.flat.view(1, -1)
+        self._arena = arena  # P is read from it at every use: the parameter set may be relocated
         self.G = arena.grad_set if hasattr(arena, "grad_set") else arena.grad_flat.view(1, -1)
         self.K, self.ld = self.P.shape
         dev = self.P.device
@@ -154,6 +154,12 @@ class ArenaAdam(torch.optim.Optimizer):
         self._placed = None  # the candidate buffer holding M and V once _place chose one
         self.placement = None  # the placement record (probe times, or why it was skipped)
         self.place_opt = placement  # False: never probe / move the moments (gym_amd.placement.policy)
+
+    @property
+    def P(self):
+        """The parameter set [K, ld] (the replica arena's rows, or the node's arena as one row)."""
+        a = self._arena
+        return a.flat_set if hasattr(a, "flat_set") else a.flat.view(1, -1)
 
     @property
     def M(self):

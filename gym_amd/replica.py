@@ -138,6 +138,8 @@ class ReplicaRunner:
                 if hp is not None:
                     self.outer = DiLoCoOuter(self.coll, self.K, ld, dev, dt, placement=s.placement_opt, **hp)
                     self.outer.init_master(self.ra.flat_set[0])
+                    # the step may move the replica set itself (every model re-pointed)
+                    self.outer.relocate_replicas = self.ra.relocate_params
                 else:
                     # any other outer OptimSpec (diloco.py:26-28): torch's optimizer on an fp32
                     # master of node 0's start (diloco.py:81-89), fed the node average

@@ -520,6 +520,7 @@ def test_placement_false_bit_identical_without_probe_launches(monkeypatch):
         opt = ArenaAdam(ra.params, ra, lr=1e-3, weight_decay=0.01, placement=placed)
         eng = E.DiLoCoOuter(Collective(), 4, ra.ld, DEV, torch.float32, placement=placed)
         eng.init_master(ra.flat_set[0])
+        eng.relocate_replicas = ra.relocate_params  # as ReplicaRunner: the step may move the replica set
         g = torch.Generator(device=DEV)
         g.manual_seed(5)
         for _ in range(2):
@@ -536,12 +537,16 @@ def test_placement_false_bit_identical_without_probe_launches(monkeypatch):
             for p in model.parameters():
                 p.grad.copy_(torch.randn(p.shape, device=DEV, generator=g) * 1e-2)
             dm.step()
+        ra.check_bound()  # every model still reads its row of the (possibly moved) parameter set
+        lo, hi = ra.flat_set.data_ptr(), ra.flat_set.data_ptr() + 4 * ra.flat_set.numel()
+        assert all(lo <= p.data_ptr() < hi for p in ra.params)
         out = [t.clone() for t in (ra.flat_set, eng.master, eng.mom, opt.M, opt.V)]
         out += [p.detach().clone() for p in model.parameters()]
         return out, (opt.placement, eng.placement, dm.placement)
 
     placed, recs_on = run(True)
     assert recs_on[1] is not None and recs_on[1].get("candidates", 0) >= 2
+    assert recs_on[1]["replica_set"]["candidates"] >= 2, recs_on[1]
 
     def boom(*a, **k):
         raise AssertionError("placement probe launched with placement=False")

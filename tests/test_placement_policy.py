@@ -4,6 +4,7 @@ strategies record the option in __config__()."""
 import os
 import sys
 
+import pytest
 import torch
 import torch.distributed as dist
 
@@ -44,3 +45,42 @@ def test_strategy_config_records_the_option():
     cfg = s.__config__()
     assert cfg["placement"] == {"enabled": False, "records": {}}
     assert SimpleReduceStrategy().__config__()["placement"]["enabled"] is True
+
+
+def test_replica_arena_relocate_params():
+    """ReplicaArena.relocate_params (DiLoCoOuter's replica-set stage, through
+    ReplicaRunner): the K rows move into the new buffer with their values,
+    every model's parameters read the new rows, the gradients stay bound, and
+    ArenaAdam (which reads the set from the arena) steps the moved rows."""
+    import copy
+
+    from gym_amd.arena import ReplicaArena, ReplicaSet
+    torch.manual_seed(0)
+    models = [torch.nn.Linear(6, 5) for _ in range(3)]
+    for k, m in enumerate(models):
+        with torch.no_grad():
+            m.weight.add_(k)
+    ra = ReplicaArena(models)
+    before = [copy.deepcopy(m.state_dict()) for m in models]
+    gptr = [p.grad.data_ptr() for p in ra.params]
+    new = torch.full_like(ra.flat_set, float("nan"))
+    ra.relocate_params(new)
+    assert ra.flat_set is new
+    ra.check_bound()
+    lo, hi = new.data_ptr(), new.data_ptr() + 4 * new.numel()
+    assert all(lo <= p.data_ptr() < hi for p in ra.params)
+    assert [p.grad.data_ptr() for p in ra.params] == gptr
+    for m, b in zip(models, before):
+        for key, v in m.state_dict().items():
+            assert torch.equal(v, b[key])
+    with torch.no_grad():
+        models[1].bias.fill_(7.0)  # a write through the model lands in the new set
+    assert (new[1, ra.layout.offsets[1]:ra.layout.offsets[1] + 5] == 7.0).all()
+    with pytest.raises(ValueError):
+        ra.relocate_params(torch.zeros(2, ra.ld))
+    rs = ReplicaSet(ra.layout, 2, "cpu")
+    rs.data.normal_()
+    keep = rs.data.clone()
+    other = torch.zeros_like(rs.data)
+    rs.relocate(other)
+    assert rs.data is other and torch.equal(other, keep)
