@@ -78,3 +78,42 @@ def test_replica_forward_vmap_matches_loop_gpu(strategy):
         pytest.skip("no GPU")
     from test_replica_vmap import _train, assert_states_close
     assert_states_close(_train("loop", "cuda:0", strategy), _train("vmap", "cuda:0", strategy))
+
+
+def test_diloco_replica_set_relocation_in_the_replica_loop():
+    """ReplicaRunner with DiLoCo at a size where placement runs (9.4M parameters
+    per node, K = 4): the outer step may move the replica set itself
+    (ReplicaArena.relocate_params); the nodes end bit-identical to
+    placement=False, every model reads its row of the current set, and the
+    fused AdamW steps the moved rows."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from strategy_scenarios import ShapeModel
+    from gym_amd.replica import ReplicaRunner
+    from gym_amd.strategy import DiLoCoStrategy, OptimSpec
+    shapes = [(2048, 2048), (2048, 2048), (1024, 1024), (300,)]
+
+    def run(placed):
+        torch.manual_seed(3)
+        models = [ShapeModel(shapes, seed=5).to("cuda:0") for _ in range(4)]
+        s = DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-3), H=2, placement=placed)
+        runner = ReplicaRunner(s, models, rank=0, num_nodes=4)
+        g = torch.Generator(device="cuda:0").manual_seed(11)
+        for _ in range(5):
+            runner.zero_grad()
+            for m in models:
+                for p in m.parameters():
+                    p.grad.copy_(torch.randn(p.shape, device="cuda:0", generator=g) * 1e-2)
+            runner.step()
+        ra = runner.ra
+        ra.check_bound()
+        lo, hi = ra.flat_set.data_ptr(), ra.flat_set.data_ptr() + 4 * ra.flat_set.numel()
+        assert all(lo <= p.data_ptr() < hi for p in ra.params)
+        return [p.detach().clone() for m in models for p in m.parameters()], runner.outer.placement
+
+    placed, rec = run(True)
+    assert rec is not None and rec.get("replica_set", {}).get("candidates", 0) >= 2, rec
+    plain, rec_off = run(False)
+    assert rec_off == {"placed": False, "why": "placement=False"}
+    for a, b in zip(placed, plain):
+        assert torch.equal(a, b)
