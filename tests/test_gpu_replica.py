@@ -69,7 +69,7 @@ def test_replica_eval_average_gpu():
     assert np.array_equal(avg, mean_reduce(list(rows)))  # ascending in-kernel sum, true division: bit-exact
 
 
-@pytest.mark.parametrize("strategy", ["simple", "sparta", "diloco"])
+@pytest.mark.parametrize("strategy", ["simple", "sparta", "diloco", "fedavg"])
 def test_replica_forward_vmap_matches_loop_gpu(strategy):
     """replica_forward="vmap" (one torch.func.vmap over the arena rows, BatchNorm
     and causal SDPA in the model) trains K = 3 nodes with the HIP kernels to the
