@@ -124,8 +124,7 @@ class ArenaAdam(torch.optim.Optimizer):
         if len(self.param_groups) != 1:
             raise ValueError("ArenaAdam: one parameter group (the node's arena)")
         self.arenas = list(getattr(arena, "arenas", [arena]))
-        self._arena = arena  # P is read from it at every use: the parameter set may be relocated
-        self.G = arena.grad_set if hasattr(arena, "grad_set") else arena.grad_flat.view(1, -1)
+        self._arena = arena  # P and G are read from it at every use: the sets may be relocated
         self.K, self.ld = self.P.shape
         dev = self.P.device
         self._M = torch.zeros_like(self.P, dtype=torch.float32)
@@ -160,6 +159,12 @@ class ArenaAdam(torch.optim.Optimizer):
         """The parameter set [K, ld] (the replica arena's rows, or the node's arena as one row)."""
         a = self._arena
         return a.flat_set if hasattr(a, "flat_set") else a.flat.view(1, -1)
+
+    @property
+    def G(self):
+        """The gradient set, read from the arena like P."""
+        a = self._arena
+        return a.grad_set if hasattr(a, "grad_set") else a.grad_flat.view(1, -1)
 
     @property
     def M(self):
