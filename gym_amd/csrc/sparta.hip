@@ -593,6 +593,14 @@ constexpr int kWTile = 64 * kSpPerThread * kWGroups;  // elements per wavefront 
 constexpr int kWList = 256;                // listed positions per window
 constexpr int kSpWaves = 4;  // wavefronts (independent tiles) per workgroup
 
+// x / d as torch's true division; a power-of-two d (K = 4, 8, 16, 32, 64 nodes) is
+// an exact scaling, so the reciprocal multiply gives the same bits in one VALU
+// instead of the ~10 of the IEEE division sequence (uniform branch)
+__device__ __forceinline__ float div_nodes(float x, float d) {
+    if ((__float_as_uint(d) & 0x807fffffu) == 0u && d != 0.f) return x * (1.f / d);
+    return x / d;
+}
+
 // orders this wave's LDS accesses (the wave is the only writer of its slices)
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -723,7 +731,7 @@ struct WaveBatchDpp2 {
                 for (int j = 0; j < VPL; ++j) c = (((c + f[j][0]) + f[j][1]) + f[j][2]) + f[j][3];
                 a = q == s ? c : a;
             }
-            const float avg = __shfl(a / divisor, (lane & ~(LQ - 1)) | (LQ - 1), 64);
+            const float avg = __shfl(div_nodes(a, divisor), (lane & ~(LQ - 1)) | (LQ - 1), 64);
             if (e < ne) {
                 const float w[4] = {avg, avg, avg, avg};
                 V* p = reinterpret_cast<V*>(src + (tile0 + list[b0 + e]) * ld + 4 * VPL * q);
