@@ -591,6 +591,9 @@ def bench_simple(args, coll, dev, K_total=8, model="gpt2-char"):
     layout.n = layout.padded_to(coll.world)
     rs = synth_replicas(layout, K, coll.rank, dev)
     eng = MeanReduce(coll, K, layout.n, dev, torch.float32)
+    # as the replica loop does: the mean may move the set it averages into the memory it
+    # runs fastest on, once, at its first call (MeanReduce._place; sets of >= 32 MB per row)
+    eng.relocate_replicas = rs.relocate
     t = timed_loop(lambda: eng(rs.data), args.steps, args.warmup, coll)
     out = {"ms_per_step": round(t * 1e3, 4), "param_GBps": round(K * coll.world * 4 * numel(shapes) / t / 1e9, 1),
            "K_local": K, "K_total": K * coll.world, "model": model}
@@ -616,6 +619,10 @@ def bench_simple(args, coll, dev, K_total=8, model="gpt2-char"):
         alg = 2 * K * 4 * layout.n
         out.update({"kernel_ms": round(q, 4), "kernel_alg_GBps": round(alg / (q * 1e-3) / 1e9, 1),
                     "kernel_frac_hbm": round(alg / (q * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        pl = eng.placement
+        if pl and pl.get("probe_ms"):
+            out["placement"] = {"candidates": pl["candidates"], "chosen": pl["chosen"],
+                                "probe_ms_own_vs_best": [pl["probe_ms"][0], min(pl["probe_ms"])]}
     return out
 
 
@@ -946,6 +953,8 @@ def main():
                   ("sparta_k32_torch_mask", lambda a, c, d: bench_sparta(a, c, d, mask_source="torch")),
                   ("sparta_k32_replica_step", bench_sparta_replica_step),
                   ("simple_reduce_char_k8", bench_simple),
+                  # the same mean over GPT-2 124M gradients (SimpleReduce / FedAvg in the replica loop)
+                  ("simple_reduce_124m_k8", lambda a, c, d: bench_simple(a, c, d, model="gpt2-124m")),
                   ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
     if args.only and args.only != "diloco":
         fn = {"sparta": bench_sparta, "simple": bench_simple, "demo": bench_demo,

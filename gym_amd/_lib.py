@@ -61,6 +61,7 @@ SIGNATURES = {
     "ga_probe_philox": (c_i32, [c_i64, c_p, c_p]),
     "ga_probe_chunk_stream": (c_i32, [c_p, c_p, c_i64, c_i64, c_i32, c_p]),
     "ga_probe_diloco_placement": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "ga_probe_mean_placement": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p]),
     "ga_probe_adam_placement": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p]),
     "ga_replica_mean": (c_i32, [c_i32, c_p, c_i64, c_i64, c_p, c_i64, c_f32, c_p, c_i64, c_i64, c_p]),
     "ga_diloco_outer": (c_i32, [c_i32, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p, c_i32, c_i32, c_f32, c_f32,

@@ -234,6 +234,22 @@ class ReplicaArena:
         for a in self.arenas:
             a.sync_grads()
 
+    def relocate_grads(self, grad_set):
+        """Move the K gradient rows into another [K, ld] buffer (contents copied;
+        every model's .grad re-pointed at its view of the new rows): how the
+        SimpleReduce step moves the gradient set into the memory its mean runs
+        fastest on (engine.MeanReduce._place)."""
+        if self.grad_set is None or grad_set.shape != self.grad_set.shape or grad_set.dtype != self.grad_set.dtype:
+            raise ValueError("ReplicaArena.relocate_grads: a buffer of the gradient set's shape and dtype")
+        with torch.no_grad():
+            if grad_set.data_ptr() != self.grad_set.data_ptr():
+                grad_set.copy_(self.grad_set)
+            self.grad_set = grad_set
+            for k, a in enumerate(self.arenas):
+                a.grad_flat = grad_set[k]
+                a._grad_views = a.layout.views(grad_set[k])
+                a.rebind_grads()
+
     def relocate_params(self, flat_set):
         """Move the K parameter rows into another [K, ld] buffer (contents copied;
         every model's parameters re-pointed at their views of the new rows;

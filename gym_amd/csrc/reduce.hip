@@ -171,6 +171,24 @@ __global__ __launch_bounds__(kBlock) void diloco_probe_kernel(float* src, int64_
     }
 }
 
+// Placement probe of the in-place replica mean (no reference counterpart): the access
+// pattern of replica_mean_kernel<float, true> with dst == src -- workgroup b's block of
+// the K replica streams loaded, then stored back non-temporally -- with every value
+// written back unchanged.  K <= kProbeK.
+__global__ __launch_bounds__(kBlock) void mean_probe_kernel(float* src, int64_t K, int64_t ld_src, int64_t n) {
+    int64_t lo, hi;
+    chunk_range(n >> 2, lo, hi);
+    for (int64_t v = lo + threadIdx.x; v < hi; v += kBlock) {
+        float4 x[kProbeK];
+#pragma unroll
+        for (int k = 0; k < kProbeK; ++k)
+            if (k < K) x[k] = stream_load(reinterpret_cast<const float4*>(src + k * ld_src) + v);
+#pragma unroll
+        for (int k = 0; k < kProbeK; ++k)
+            if (k < K) stream_store(reinterpret_cast<float4*>(src + k * ld_src) + v, x[k]);
+    }
+}
+
 static bool aligned(const void* p, int bytes) { return p == nullptr || ((uintptr_t)p % bytes) == 0; }
 
 template <typename T>
@@ -290,4 +308,16 @@ extern "C" GA_API int ga_probe_diloco_placement(float* src, int64_t K, int64_t l
     hipLaunchKernelGGL(diloco_probe_kernel, dim3(chunk_grid(n / 4)), dim3(kBlock), 0, stream, src, K, ld_src, n,
                        master, mom);
     return check_launch("ga_probe_diloco_placement");
+}
+
+extern "C" GA_API int ga_probe_mean_placement(float* src, int64_t K, int64_t ld_src, int64_t n, hipStream_t stream) {
+    clear_error();
+    GA_REQUIRE(n >= 0 && n % 4 == 0 && K >= 1 && K <= kProbeK, "ga_probe_mean_placement: bad sizes n=%lld K=%lld "
+               "(n a multiple of 4, K <= %d)", (long long)n, (long long)K, kProbeK);
+    if (n == 0) return GA_OK;
+    GA_REQUIRE(src != nullptr, "ga_probe_mean_placement: null buffer");
+    GA_REQUIRE(K == 1 || (ld_src >= n && ld_src % 4 == 0), "ga_probe_mean_placement: bad ld_src");
+    GA_REQUIRE(aligned(src, 16), "ga_probe_mean_placement: alignment");
+    hipLaunchKernelGGL(mean_probe_kernel, dim3(chunk_grid(n / 4)), dim3(kBlock), 0, stream, src, K, ld_src, n);
+    return check_launch("ga_probe_mean_placement");
 }

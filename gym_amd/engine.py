@@ -133,9 +133,16 @@ class MeanReduce:
     and overlaps the exchange of the next chunk; the same bytes on the wire as
     one all-reduce).  gloo: all-reduce of the (locally pre-summed) arena."""
 
-    def __init__(self, coll: Collective, K_local, n, device, dtype, shard=None, chunks=None):
+    def __init__(self, coll: Collective, K_local, n, device, dtype, shard=None, chunks=None, placement=True):
         self.coll, self.K_local, self.n = coll, int(K_local), int(n)
         self.K_total = coll.world * self.K_local
+        # relocate_replicas(new): moves the caller's [K, ld] set into `new` (contents copied, the
+        # caller's views re-pointed); set by the replica loop, None: the set stays where it is
+        self.relocate_replicas = None
+        self.place_opt = placement
+        self.placement = None  # the placement probe's record
+        self._placed_for = None
+        self._reps_placed = None
         W, X = coll.world, coll.exchange
         self.shard = default_shard(coll, self.n, dtype) if shard is None else bool(shard and X)
         if self.shard:
@@ -147,10 +154,54 @@ class MeanReduce:
     def _divide(self, rs_shard, m, own):
         ops.replica_mean(rs_shard, own, divisor=self.K_total)
 
+    def _place(self, reps):
+        """Once per replica set, single process: the in-place mean runs 1.49 or
+        1.26 ms at GPT-2 124M x 8 depending on where the set sits physically
+        (profiles/r05y_mean_placement.txt), so when the caller can move it
+        (relocate_replicas) up to REPLICA_PLACEMENT_CANDIDATES fresh [K, ld] sets
+        are timed with ga_probe_mean_placement (the step's access pattern, every
+        value written back unchanged) and the set moves to the fastest when it
+        beats its own time.  Returns the set to use from now on."""
+        key = (reps.data_ptr(), reps.stride(0))
+        if self._placed_for == key or self.relocate_replicas is None:
+            return reps
+        self._placed_for = key
+        from . import placement
+        ok, why = placement.policy(self.place_opt)
+        if not ok:
+            self.placement = {"placed": False, "why": why}
+            return reps
+        K, ld = reps.shape
+        if (reps.device.type != "cuda" or reps.dtype != torch.float32 or not reps.is_contiguous() or K > 16
+                or 4 * ld < SHARD_MIN_BYTES or self.n % 4 or ld % 4 or REPLICA_PLACEMENT_CANDIDATES < 2):
+            return reps
+
+        def as_set(buf):
+            return buf.tensor()[:K * ld].view(K, ld)
+
+        def probe(t):
+            return placement.time_probe(lambda: ops.probe_mean_placement(t, self.n))
+
+        best_buf, times = placement.choose(4 * K * ld, reps.device, lambda b: probe(as_set(b)), probe(reps),
+                                           REPLICA_PLACEMENT_CANDIDATES, PLACEMENT_MAX_FRAC)
+        best = 0
+        if best_buf is not None:
+            best = min(range(len(times)), key=lambda i: times[i])
+            new = as_set(best_buf)
+            self.relocate_replicas(new)
+            self._reps_placed = best_buf
+            reps = new
+            self._placed_for = (reps.data_ptr(), reps.stride(0))
+        self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
+                          "how": "the caller's replica set moved to the fastest of fresh [K, ld] allocations; "
+                                 "candidate 0 = where it was"}
+        return reps
+
     def __call__(self, reps):
         K, n = self.K_local, self.n
         if not self.coll.exchange:
             if K > 1:
+                reps = self._place(reps)
                 ops.replica_mean(reps, reps, n=n)
             return
         if self.shard:

@@ -422,6 +422,17 @@ def probe_diloco_placement(reps, n, master, mom):
           "ga_probe_diloco_placement")
 
 
+def probe_mean_placement(reps, n):
+    """The in-place ga_replica_mean's access pattern over fp32 replicas [K, ld]
+    (K <= 16), every value written back unchanged (placement probe)."""
+    r2 = _as2d(reps)
+    _gpu(r2)
+    K, ld = _rows_ld(r2)
+    if r2.dtype != torch.float32:
+        raise ValueError("probe_mean_placement: fp32 buffers")
+    check(lib().ga_probe_mean_placement(_p(r2), K, ld, int(n), _stream()), "ga_probe_mean_placement")
+
+
 def probe_adam_placement(param, grad, exp_avg, exp_avg_sq):
     """ga_adam_step's access pattern over fp32 [K, ld] sets of one layout, every
     value written back unchanged (placement probe)."""

@@ -152,7 +152,11 @@ class ReplicaRunner:
             self.islands = (isinstance(s, FedAvgStrategy) and s.island_size is not None
                             and s.island_size < num_nodes)
             if isinstance(s, (SimpleReduceStrategy, FedAvgStrategy)) and not self.islands:
-                self.mean = MeanReduce(self.coll, self.K, ld, dev, dt)
+                self.mean = MeanReduce(self.coll, self.K, ld, dev, dt, placement=s.placement_opt)
+                # the mean may move the set it averages (gradients for SimpleReduce, parameters for
+                # FedAvg) into the memory it runs fastest on, once (MeanReduce._place)
+                self.mean.relocate_replicas = (self.ra.relocate_grads if isinstance(s, SimpleReduceStrategy)
+                                               else self.ra.relocate_params)
             if self.islands:
                 self._isl_row = torch.empty(1, ld, device=dev, dtype=dt)
                 self._isl_all = None  # [num_nodes, ld]: every node's parameters, gathered (processes > 1)

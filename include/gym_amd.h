@@ -142,6 +142,17 @@ GA_API int ga_probe_diloco_placement(float* src, int64_t K, int64_t ld_src, int6
                                      hipStream_t stream);
 
 /*
+ * Placement probe (no reference counterpart) for the in-place replica mean
+ * (ga_replica_mean with dst == src, the SimpleReduce / FedAvg step over K local
+ * replicas): its access pattern over an fp32 [K, ld_src] set (K <= 16, n a
+ * multiple of 4) with every value written back unchanged.  The in-place mean over
+ * GPT-2 124M x 8 runs 1.49 ms in an ordinary allocation and 1.26 ms in the
+ * fastest of 12 fresh ones (profiles/r05y_mean_placement.txt); MeanReduce times
+ * candidate sets with this probe once and moves the caller's set to the fastest.
+ */
+GA_API int ga_probe_mean_placement(float* src, int64_t K, int64_t ld_src, int64_t n, hipStream_t stream);
+
+/*
  * Placement probe (no reference counterpart) for the fused Adam/AdamW step:
  * ga_adam_step's access pattern over fp32 [K, ld] param / grad / exp_avg /
  * exp_avg_sq sets (n a multiple of 4, 16-byte aligned) -- p, g, m, v read, p, m,

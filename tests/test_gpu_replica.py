@@ -80,24 +80,31 @@ def test_replica_forward_vmap_matches_loop_gpu(strategy):
     assert_states_close(_train("loop", "cuda:0", strategy), _train("vmap", "cuda:0", strategy))
 
 
-def test_diloco_replica_set_relocation_in_the_replica_loop():
-    """ReplicaRunner with DiLoCo at a size where placement runs (9.4M parameters
-    per node, K = 4): the outer step may move the replica set itself
-    (ReplicaArena.relocate_params); the nodes end bit-identical to
-    placement=False, every model reads its row of the current set, and the
-    fused AdamW steps the moved rows."""
+@pytest.mark.parametrize("name", ["diloco", "simple", "fedavg"])
+def test_replica_set_relocation_in_the_replica_loop(name):
+    """ReplicaRunner at a size where placement runs (9.4M parameters per node,
+    K = 4): the DiLoCo outer step may move the parameter set, SimpleReduce's mean
+    the gradient set, FedAvg's mean the parameter set (ReplicaArena.relocate_params
+    / relocate_grads); the nodes end bit-identical to placement=False, every model
+    reads its row of the current sets, and the fused AdamW steps the moved rows."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from strategy_scenarios import ShapeModel
     from gym_amd.replica import ReplicaRunner
-    from gym_amd.strategy import DiLoCoStrategy, OptimSpec
+    from gym_amd.strategy import DiLoCoStrategy, FedAvgStrategy, OptimSpec, SimpleReduceStrategy
     shapes = [(2048, 2048), (2048, 2048), (1024, 1024), (300,)]
+
+    def strategy(placed):
+        if name == "diloco":
+            return DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-3), H=2, placement=placed)
+        if name == "simple":
+            return SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-3), placement=placed)
+        return FedAvgStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.05), H=2, placement=placed)
 
     def run(placed):
         torch.manual_seed(3)
         models = [ShapeModel(shapes, seed=5).to("cuda:0") for _ in range(4)]
-        s = DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-3), H=2, placement=placed)
-        runner = ReplicaRunner(s, models, rank=0, num_nodes=4)
+        runner = ReplicaRunner(strategy(placed), models, rank=0, num_nodes=4)
         g = torch.Generator(device="cuda:0").manual_seed(11)
         for _ in range(5):
             runner.zero_grad()
@@ -107,12 +114,15 @@ def test_diloco_replica_set_relocation_in_the_replica_loop():
             runner.step()
         ra = runner.ra
         ra.check_bound()
-        lo, hi = ra.flat_set.data_ptr(), ra.flat_set.data_ptr() + 4 * ra.flat_set.numel()
-        assert all(lo <= p.data_ptr() < hi for p in ra.params)
-        return [p.detach().clone() for m in models for p in m.parameters()], runner.outer.placement
+        for buf, ts in ((ra.flat_set, [p.data for p in ra.params]), (ra.grad_set, [p.grad for p in ra.params])):
+            lo, hi = buf.data_ptr(), buf.data_ptr() + 4 * buf.numel()
+            assert all(lo <= t.data_ptr() < hi for t in ts)
+        rec = runner.outer.placement if name == "diloco" else runner.mean.placement
+        return [p.detach().clone() for m in models for p in m.parameters()], rec
 
     placed, rec = run(True)
-    assert rec is not None and rec.get("replica_set", {}).get("candidates", 0) >= 2, rec
+    cand = rec.get("replica_set", rec) if rec else {}
+    assert cand.get("candidates", 0) >= 2, rec
     plain, rec_off = run(False)
     assert rec_off == {"placed": False, "why": "placement=False"}
     for a, b in zip(placed, plain):
