@@ -124,6 +124,10 @@ class ReplicaRunner:
                                     chunk=kw["compression_chunk"], topk=kw["compression_topk"],
                                     bf16_transform=kw.get("bf16_transform", "fp32") if dt == torch.bfloat16
                                     else "fp32")
+            # after the first step the [K, ld] parameter, gradient and delta sets may move into
+            # the memory the K-row encode + decode run fastest on, as the DeMo optimizer's own
+            # (_place_demo; placement=False keeps them where they are)
+            self.placement, self._placed = None, None
         else:
             spec = s.optim_spec if isinstance(s, SimpleReduceStrategy) else s.inner_optim_spec
             if fusable(spec.cls, spec.kwargs, self.ra):
@@ -194,6 +198,8 @@ class ReplicaRunner:
             lr = self.optim.param_groups[0]["lr"]
             kw = self.demo_kw
             self.codec(P, G, self.delta, lr, kw["compression_decay"], kw["weight_decay"])
+            if self.placement is None:
+                self._place_demo(P, G, lr)
         elif isinstance(s, SimpleReduceStrategy):
             self.ra.sync_grads()
             self.mean(G)
@@ -225,6 +231,31 @@ class ReplicaRunner:
             for cb in s.lr_callbacks:
                 cb(self.lr_scheds[0].get_last_lr()[0])
         s.local_step += 1
+
+    def _place_demo(self, P, G, lr):
+        """Once, after the first DeMo step: the K nodes' parameter, gradient and
+        delta sets into the fresh device allocations the step's encode + decode
+        run fastest on (engine.place_demo_step over [K, ld] sets, as
+        demo_impl.demo.DeMo._place does for one node; the probe restores all
+        three, so the nodes' steps are unchanged).  Every model's parameters and
+        gradients are re-pointed at their rows of the moved sets
+        (ReplicaArena.relocate_params / relocate_grads; the caller contract of
+        INTEGRATION.md applies)."""
+        from .placement import policy
+        ok, why = policy(self.demo_kw.get("placement", True))
+        if not ok:
+            self.placement = {"placed": False, "why": why}
+            return
+        bufs, tens, rec = self.codec.place(P, G, self.delta, lr, self.demo_kw["compression_decay"])
+        self.placement = rec or {"placed": False}
+        if bufs is None or tens is None or not any(b is not None for b in bufs):
+            return
+        if tens[0].data_ptr() != P.data_ptr():
+            self.ra.relocate_params(tens[0])
+        if tens[1].data_ptr() != G.data_ptr():
+            self.ra.relocate_grads(tens[1])
+        self.delta = tens[2]
+        self._placed = bufs  # own the memory the sets now live in
 
     def _generic_outer(self, P):
         """DiLoCo's outer step for a non-SGD outer optimizer (diloco.py:34-49,

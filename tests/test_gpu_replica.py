@@ -80,18 +80,19 @@ def test_replica_forward_vmap_matches_loop_gpu(strategy):
     assert_states_close(_train("loop", "cuda:0", strategy), _train("vmap", "cuda:0", strategy))
 
 
-@pytest.mark.parametrize("name", ["diloco", "simple", "fedavg"])
+@pytest.mark.parametrize("name", ["diloco", "simple", "fedavg", "demo"])
 def test_replica_set_relocation_in_the_replica_loop(name):
     """ReplicaRunner at a size where placement runs (9.4M parameters per node,
     K = 4): the DiLoCo outer step may move the parameter set, SimpleReduce's mean
-    the gradient set, FedAvg's mean the parameter set (ReplicaArena.relocate_params
-    / relocate_grads); the nodes end bit-identical to placement=False, every model
+    the gradient set, FedAvg's mean the parameter set, the DeMo step all three of
+    its parameter, gradient and delta sets (ReplicaArena.relocate_params /
+    relocate_grads); the nodes end bit-identical to placement=False, every model
     reads its row of the current sets, and the fused AdamW steps the moved rows."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from strategy_scenarios import ShapeModel
     from gym_amd.replica import ReplicaRunner
-    from gym_amd.strategy import DiLoCoStrategy, FedAvgStrategy, OptimSpec, SimpleReduceStrategy
+    from gym_amd.strategy import DeMoStrategy, DiLoCoStrategy, FedAvgStrategy, OptimSpec, SimpleReduceStrategy
     shapes = [(2048, 2048), (2048, 2048), (1024, 1024), (300,)]
 
     def strategy(placed):
@@ -99,6 +100,8 @@ def test_replica_set_relocation_in_the_replica_loop(name):
             return DiLoCoStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-3), H=2, placement=placed)
         if name == "simple":
             return SimpleReduceStrategy(optim_spec=OptimSpec(torch.optim.AdamW, lr=1e-3), placement=placed)
+        if name == "demo":
+            return DeMoStrategy(lr=1e-3, placement=placed)
         return FedAvgStrategy(inner_optim=OptimSpec(torch.optim.SGD, lr=0.05), H=2, placement=placed)
 
     def run(placed):
@@ -117,12 +120,15 @@ def test_replica_set_relocation_in_the_replica_loop(name):
         for buf, ts in ((ra.flat_set, [p.data for p in ra.params]), (ra.grad_set, [p.grad for p in ra.params])):
             lo, hi = buf.data_ptr(), buf.data_ptr() + 4 * buf.numel()
             assert all(lo <= t.data_ptr() < hi for t in ts)
-        rec = runner.outer.placement if name == "diloco" else runner.mean.placement
+        rec = {"diloco": lambda: runner.outer.placement, "demo": lambda: runner.placement}.get(
+            name, lambda: runner.mean.placement)()
+        if name == "demo" and runner._placed is not None and runner._placed[2] is not None:
+            assert runner.delta.data_ptr() == runner._placed[2].tensor().data_ptr()  # the step's delta moved too
         return [p.detach().clone() for m in models for p in m.parameters()], rec
 
     placed, rec = run(True)
     cand = rec.get("replica_set", rec) if rec else {}
-    assert cand.get("candidates", 0) >= 2, rec
+    assert max(cand.get("candidates", 0), cand.get("candidates_per_buffer", 0)) >= 2, rec
     plain, rec_off = run(False)
     assert rec_off == {"placed": False, "why": "placement=False"}
     for a, b in zip(placed, plain):
