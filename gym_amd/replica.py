@@ -304,8 +304,15 @@ class ReplicaRunner:
             if not mine:
                 continue
             ops.replica_mean(src, self._isl_row, rows=rows, divisor=float(len(members)))
-            for m in mine:
-                ops.replica_mean(self._isl_row, P[m - lo:m - lo + 1], divisor=1.0)
+            # written back in one launch per run of consecutive member rows (members ascend)
+            r0 = prev = mine[0]
+            for m in mine[1:] + [None]:
+                if m is not None and m == prev + 1:
+                    prev = m
+                    continue
+                ops.replica_mean(self._isl_row, P[r0 - lo:prev - lo + 1], divisor=1.0)
+                if m is not None:
+                    r0 = prev = m
 
     def _grad_less(self):
         """Indices of node 0's tensors without a gradient (skipped, sparta.py:29-30)."""
