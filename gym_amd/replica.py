@@ -48,6 +48,17 @@ from .strategy.sparta import MaskDraw, RandomIndexSelector, SPARTAStrategy, draw
 from .strategy.strategy import SimpleReduceStrategy, clip_arena_grad_norm_
 
 
+def consecutive_runs(xs):
+    """[(first, last)] of the runs of consecutive integers in ascending xs."""
+    runs = []
+    for x in xs:
+        if runs and x == runs[-1][1] + 1:
+            runs[-1][1] = x
+        else:
+            runs.append([x, x])
+    return [tuple(r) for r in runs]
+
+
 class _LRGroup(torch.optim.Optimizer):
     """Holds the learning rate a scheduler drives when the step itself is a
     kernel (DeMo): one group with one placeholder parameter, no state."""
@@ -304,15 +315,9 @@ class ReplicaRunner:
             if not mine:
                 continue
             ops.replica_mean(src, self._isl_row, rows=rows, divisor=float(len(members)))
-            # written back in one launch per run of consecutive member rows (members ascend)
-            r0 = prev = mine[0]
-            for m in mine[1:] + [None]:
-                if m is not None and m == prev + 1:
-                    prev = m
-                    continue
-                ops.replica_mean(self._isl_row, P[r0 - lo:prev - lo + 1], divisor=1.0)
-                if m is not None:
-                    r0 = prev = m
+            # written back in one launch per run of consecutive member rows
+            for a0, a1 in consecutive_runs(mine):
+                ops.replica_mean(self._isl_row, P[a0 - lo:a1 - lo + 1], divisor=1.0)
 
     def _grad_less(self):
         """Indices of node 0's tensors without a gradient (skipped, sparta.py:29-30)."""

@@ -71,6 +71,15 @@ def test_replica_layout_rules():
         replica_layout(8, [0], 4, s)  # 2 processes on 1 GPU
 
 
+def test_consecutive_runs():
+    """FedAvg islands write the island mean back once per run of consecutive member rows."""
+    from gym_amd.replica import consecutive_runs
+    assert consecutive_runs([]) == []
+    assert consecutive_runs([4]) == [(4, 4)]
+    assert consecutive_runs([0, 1, 2]) == [(0, 2)]
+    assert consecutive_runs([0, 2, 3, 5, 6, 7, 9]) == [(0, 0), (2, 3), (5, 7), (9, 9)]
+
+
 def test_replica_eval_average(fake):
     from oracle.reduce import mean_reduce
     avg, rows = R.replica_eval_average(3, "cpu", True)
