@@ -4,7 +4,7 @@ round 5).  The parent never touches the GPU: it starts `python tools/exp_diloco_
 replica_placement.py --child on|off` processes alternately; each child sets the
 constant (off: 0) and runs bench.py's main (--no-extras --no-cpu-baseline --no-pmc),
 and the parent prints one JSON line per child: kernel ms, frac, the replica-set and
-master probe minima.  Usage: python tools/exp_diloco_replica_placement.py [pairs]"""
+master probe minima.  Usage: python tools/exp_diloco_replica_placement.py [pairs] [modes: on,off or e.g. on,20]"""
 import json
 import os
 import subprocess
@@ -18,6 +18,8 @@ def child(mode):
     from gym_amd import engine
     if mode == "off":
         engine.REPLICA_PLACEMENT_CANDIDATES = 0
+    elif mode.isdigit():  # a candidate count other than the default
+        engine.REPLICA_PLACEMENT_CANDIDATES = int(mode)
     import bench
     sys.argv = ["bench.py", "--no-extras", "--no-cpu-baseline", "--no-pmc", "--steps", "20", "--warmup", "3"]
     bench.main()
@@ -25,8 +27,9 @@ def child(mode):
 
 def main():
     pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["on", "off"]
     for i in range(pairs):
-        for mode in ("on", "off"):
+        for mode in modes:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", mode], capture_output=True,
                                text=True, timeout=300, cwd=ROOT)
             lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
