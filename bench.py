@@ -2,11 +2,15 @@
 param GB/s (%HBM/xGMI peak) + ms/outer step, GPT-2 124M, 1-8 GPUs).
 
 Headline workload (configs[2]): the DiLoCo outer step of GPT-2 124M over 8
-simulated nodes per GPU (batched-replica arena [8, N] per GPU; at N GPUs the
-nodes of all GPUs are averaged: in-kernel over the local 8, RCCL across GPUs;
-weak scaling).  One timed "step" = one outer step: sum/average of every
-node's parameters, pseudo-gradient, outer Nesterov SGD, write-back into every
-node.  Inputs are synthetic, resident in HBM before timing starts.
+simulated nodes IN TOTAL, 8/N per GPU (N=1: a batched-replica arena [8, n] on
+one GPU, averaged in-kernel; N=8: one node per GPU, RCCL reduce-scatter /
+all-gather over xGMI; between, an in-kernel pre-sum over the local 8/N then
+RCCL).  Total work is fixed as N grows (scaling "strong"), so the driver's
+1->8 curve runs ONE configuration and at N=8 the headline's "xgmi" block is
+the north star's xGMI fraction.  One timed "step" = one outer step:
+sum/average of every node's parameters, pseudo-gradient, outer Nesterov SGD,
+write-back into every node.  Inputs are synthetic, resident in HBM before
+timing starts.
 
 value = node-parameter bytes averaged per second over the whole job
         = K_total * 4 * N_params / t_step  ("param GB/s"); ms_per_step = t_step.
@@ -29,8 +33,8 @@ nodes in total, 32/G per GPU, p=0.005, Philox mask: configs[3]), SimpleReduce
 (char-level nanoGPT, 8 nodes in total, 8/G per GPU: configs[1]), DeMo (GPT-2
 350M, one node per GPU, chunk 64 / top-k 32: configs[4]), the inner AdamW +
 clip step on one GPT-2 124M arena (fused vs torch foreach), and at G > 1 the
-DiLoCo step exactly as configs[2] names it -- one node per GPU, so the
-reduce-scatter/all-gather over xGMI dominates (its "xgmi" block).
+weak-scaled DiLoCo step, 8 nodes per GPU (8G in total:
+diloco_8_nodes_per_gpu).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-extras]
        torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -830,6 +834,23 @@ def bench_inner_adamw(args, coll, dev, model="gpt2-124m", max_norm=1.0):
                                                     if opt.placement and "probe_ms" in opt.placement else None)}
 
 
+def replicas_per_gpu(nodes, world, override=None):
+    """Simulated nodes each GPU hosts: `override` (--replicas) if given, else
+    the configuration's node count spread over the GPUs (8 nodes: 8 / 4 / 2 / 1
+    per GPU at N = 1 / 2 / 4 / 8), at least one.  The total is then
+    replicas x world (= nodes when world divides it)."""
+    if override:
+        return int(override)
+    if nodes % world:
+        raise SystemExit(f"--nodes {nodes} is not a multiple of {world} GPUs (give --replicas per GPU instead)")
+    return max(1, nodes // world)
+
+
+def launch_world(args):
+    """World size this process will run at: torchrun's WORLD_SIZE, else --gpus."""
+    return int(os.environ["WORLD_SIZE"]) if "WORLD_SIZE" in os.environ else args.gpus
+
+
 def free_port():
     import socket
     s = socket.socket()
@@ -881,7 +902,7 @@ def self_launch(args, argv):
     t0 = time.perf_counter()
     cpu = None
     if not args.no_cpu_baseline and args.only is None:
-        cpu = cpu_baseline_diloco(args.model, args.replicas)
+        cpu = cpu_baseline_diloco(args.model, args.nodes)
     legs["cpu_baseline_s"] = round(time.perf_counter() - t0, 1)
     cmd = child_command(argv, args.gpus, free_port())
     env = dict(os.environ)
@@ -904,7 +925,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-124m")
-    ap.add_argument("--replicas", type=int, default=8, help="simulated nodes per GPU")
+    ap.add_argument("--nodes", type=int, default=8,
+                    help="simulated nodes in total (configs[2]: 8), spread nodes/N per GPU")
+    ap.add_argument("--replicas", type=int, default=None,
+                    help="simulated nodes per GPU (overrides --nodes / N; e.g. 8 for the weak-scaled form)")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--only", default=None,
@@ -920,6 +944,7 @@ def main():
     if args.gpus > 1 and "RANK" not in os.environ and not args.pmc_child:
         sys.exit(self_launch(args, sys.argv[1:]))
     single = args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    args.replicas = replicas_per_gpu(args.nodes, launch_world(args), args.replicas)
     rank0 = int(os.environ.get("RANK", "0")) == 0
     if args.pmc_child:  # a rocprofv3 PMC pass: the headline kernel only, a few launches
         coll = setup_dist(1)
@@ -933,8 +958,8 @@ def main():
     t0 = time.perf_counter()
     if rank0 and not args.no_cpu_baseline and args.only is None:
         # at N > 1 under torchrun the other ranks wait in the rendezvous meanwhile; the
-        # baseline is the reference's configs[2] job (K gloo node processes) on this host
-        cpu = cpu_baseline_diloco(args.model, args.replicas)
+        # baseline is the reference's configs[2] job (8 gloo node processes) on this host
+        cpu = cpu_baseline_diloco(args.model, args.nodes)
     legs["cpu_baseline_s"] = round(time.perf_counter() - t0, 1)
     args.pmc = (None, "not measured (N > 1 or --no-pmc)")
     t0 = time.perf_counter()
@@ -971,13 +996,14 @@ def main():
         if coll.world == 1:
             runs.insert(0, ("diloco_torch_per_tensor_gpu",
                             lambda a, c, d: bench_diloco_torch_gpu(a, c, d, head["ms_per_step"])))
-        if coll.world > 1:  # configs[2] as named: one node per GPU, the exchange alone over xGMI
-            def diloco_1(a, c, d):
-                r = bench_diloco(argparse.Namespace(**{**vars(a), "replicas": 1}), c, d)
+        if coll.world > 1:  # the weak-scaled form: 8 nodes on every GPU (8N in total)
+            def diloco_weak(a, c, d):
+                r = bench_diloco(argparse.Namespace(**{**vars(a), "replicas": 8}), c, d)
                 for key in ("ms_per_step", "value", "kernel_ms"):
                     r[key] = round(r[key], 4)
+                r["scaling"] = "weak"
                 return r
-            runs.insert(0, ("diloco_1_node_per_gpu", diloco_1))
+            runs.insert(0, ("diloco_8_nodes_per_gpu", diloco_weak))
         for name, fn in runs:
             if coll.rank == 0:  # progress on stderr (the JSON line stays the only stdout line)
                 print(f"[bench] {name}", file=sys.stderr, flush=True)
@@ -1003,14 +1029,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(head["ms_per_step"], 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (GPT-2 124M parameter shapes, N(0,0.02) start + per-node N(0,1e-3) drift)",
-        "config": {"workload": f"DiLoCo outer step (configs[2]), {args.model}, {args.replicas} simulated nodes "
-                               f"per GPU as a batched-replica arena, {K_total} nodes total; fused "
-                               f"average+pseudo-grad+Nesterov SGD(lr=0.7, mu=0.9) + RCCL reduce-scatter/all-gather "
-                               f"across GPUs",
+        "config": {"workload": f"DiLoCo outer step (configs[2]), {args.model}, {K_total} simulated nodes in total, "
+                               f"{args.replicas} per GPU ({'a batched-replica arena, ' if args.replicas > 1 else ''}"
+                               f"fused average+pseudo-grad+Nesterov SGD(lr=0.7, mu=0.9)"
+                               f"{', RCCL reduce-scatter/all-gather across GPUs' if coll.world > 1 else ''})",
                    "model": args.model, "nodes_per_gpu": args.replicas, "nodes_total": K_total,
                    "n_params": head["n_params"], "parallelism": f"dp{K_total} (simulated nodes)"},
         "roofline": head["roofline"],

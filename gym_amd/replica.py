@@ -405,27 +405,37 @@ class _FoldedSDPA(torch.autograd.Function):
         return out.reshape(B, n, *out.shape[1:]), 0
 
 
+def _foldable(q, k, v):
+    """True when the folded call is exact: every operand carries the same
+    per-node leading dims (SDPA's own batch / heads), so node b's tokens stay in
+    node b's slice of the folded batch.  Unbatched (L, E) operands or k / v
+    broadcast over batch (a leading 1) are not foldable."""
+    return q.dim() >= 3 and k.dim() == q.dim() and v.dim() == q.dim() and \
+        q.shape[:-2] == k.shape[:-2] == v.shape[:-2]
+
+
 def _sdpa_vmappable(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False, scale=None, enable_gqa=False):
-    if attn_mask is None and dropout_p == 0.0 and not enable_gqa:
+    if attn_mask is None and dropout_p == 0.0 and not enable_gqa and _foldable(query, key, value):
         return _FoldedSDPA.apply(query, key, value, is_causal, scale)
     from torch.nn.attention import SDPBackend, sdpa_kernel
-    with sdpa_kernel([SDPBackend.MATH]):  # masks / dropout: the math backend batches under vmap
+    with sdpa_kernel([SDPBackend.MATH]):  # masks / dropout / broadcasts: the math backend batches under vmap
         return _SDPA(query, key, value, attn_mask=attn_mask, dropout_p=dropout_p, is_causal=is_causal, scale=scale,
                      enable_gqa=enable_gqa)
 
 
-@contextlib.contextmanager
-def _vmappable_attention():
-    """torch.nn.functional.scaled_dot_product_attention -> _sdpa_vmappable while
-    the batched forward runs (models that call it through the module, as
-    nanoGPT and nn.MultiheadAttention do)."""
-    F = torch.nn.functional
-    prev = F.scaled_dot_product_attention
-    F.scaled_dot_product_attention = _sdpa_vmappable
-    try:
-        yield
-    finally:
-        F.scaled_dot_product_attention = prev
+class _VmappableAttention(torch.overrides.TorchFunctionMode):
+    """Routes torch.nn.functional.scaled_dot_product_attention to
+    _sdpa_vmappable while the batched forward runs; every other torch function
+    passes through.  A torch-function mode lives on the calling thread's mode
+    stack, so only the batched forward sees it: the module attribute is never
+    swapped and another thread calling SDPA meanwhile (a data-loader worker, an
+    eval thread) gets torch's own function."""
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is _SDPA:
+            return _sdpa_vmappable(*args, **kwargs)
+        return func(*args, **kwargs)
 
 
 def _stack(batches):
@@ -451,8 +461,11 @@ class BatchedForward:
     dropout draws differ per node (randomness="different").  Scaled dot-product
     attention without mask or dropout runs as ONE fused-kernel call over the
     nodes folded into its batch dim (_FoldedSDPA; the fused kernels' backward
-    has no batching rule on this stack), with a mask or dropout on the math
-    backend.  BatchNorm under bf16 autocast does not batch (torch's vmap rule
+    has no batching rule on this stack), with a mask, dropout or operands
+    that do not fold (_foldable) on the math backend; the override is a
+    torch-function mode active only around this forward, on this thread
+    (_VmappableAttention).  The copy runs in the models' current train()/eval()
+    mode.  BatchNorm under bf16 autocast does not batch (torch's vmap rule
     for batch_norm rejects autocast's mixed dtypes): such models keep the loop.
 
     Measured on MI355X (tools/exp_replica_vmap.py, profiles/r05k_replica_vmap.txt),
@@ -500,13 +513,16 @@ class BatchedForward:
 
     def __call__(self, batches, autocast=contextlib.nullcontext):
         """batches[k]: node k's minibatch; returns the K losses (detached)."""
+        # the storage-free copy follows the models' current mode (dropout, BatchNorm), as
+        # the per-node loop does: model.train()/eval() calls on the real models never reach it
+        self.meta.train(self.models[0].training)
         losses = []
         for c0 in range(0, self.K, self.chunk):
             c1 = min(self.K, c0 + self.chunk)
             leaves = self._leaves(c0, c1)
             per_node = [dict(m.named_buffers()) for m in self.models[c0:c1]]
             bufs = {n: torch.stack([b[n] for b in per_node]) for n in self.buf_names}
-            with autocast(), _vmappable_attention():
+            with autocast(), _VmappableAttention():
                 loss = self.vloss(leaves, bufs, _stack(batches[c0:c1]))
             with warnings.catch_warnings():  # views of [K, ld] rows: strided, never the layout autograd prefers
                 warnings.filterwarnings("ignore", message=".*gradient layout contract.*")

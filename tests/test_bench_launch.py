@@ -69,7 +69,7 @@ def test_self_launch_forwards_the_child_line(monkeypatch, capsys):
 
     monkeypatch.setattr(subprocess, "run", fake_run)
     monkeypatch.setattr(bench, "cpu_baseline_diloco", lambda model, K: {"value": 1.0, "cores": 2})
-    args = bench.argparse.Namespace(gpus=2, no_cpu_baseline=False, only=None, model="gpt2-124m", replicas=8)
+    args = bench.argparse.Namespace(gpus=2, no_cpu_baseline=False, only=None, model="gpt2-124m", nodes=8, replicas=None)
     assert bench.self_launch(args, ["--gpus", "2"]) == 0
     out = capsys.readouterr().out.strip().splitlines()
     assert len(out) == 1
@@ -77,3 +77,22 @@ def test_self_launch_forwards_the_child_line(monkeypatch, capsys):
     assert line["n_gpus"] == 2 and line["cpu_baseline"] == {"value": 1.0, "cores": 2}
     assert "--nproc-per-node=2" in calls["cmd"]
     assert calls["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+@pytest.mark.parametrize("world,per_gpu", [(1, 8), (2, 4), (4, 2), (8, 1)])
+def test_headline_is_eight_nodes_in_total(world, per_gpu):
+    """configs[2] is 8 nodes in total: 8/N per GPU, so the driver's 1->8 curve
+    runs one configuration (at N = 8 one node per GPU, the exchange over xGMI)."""
+    k = bench.replicas_per_gpu(8, world)
+    assert k == per_gpu and k * world == 8
+    assert bench.replicas_per_gpu(8, world, override=8) == 8  # the weak-scaled extra
+    with pytest.raises(SystemExit):
+        bench.replicas_per_gpu(8, 3)
+
+
+def test_launch_world_prefers_torchrun_env(monkeypatch):
+    args = bench.argparse.Namespace(gpus=1)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert bench.launch_world(args) == 1
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.launch_world(args) == 4

@@ -186,3 +186,108 @@ def test_batched_forward_under_autocast():
     ra.sync_grads()
     assert ra.grad_set.abs().sum() > 0
     np.testing.assert_allclose(ra.grad_set.numpy(), g_loop.numpy(), rtol=2e-2, atol=2e-3)
+
+
+def test_sdpa_override_is_local_to_the_batched_forward():
+    """The batched forward's attention override is a torch-function mode on its
+    own thread: SDPA called from a second thread while the vmap forward runs is
+    torch's own (no folded autograd node), and the module attribute is never
+    swapped."""
+    import threading
+
+    from gym_amd.arena import ReplicaArena
+    from gym_amd.replica import BatchedForward
+    seen = {}
+
+    def other_thread():
+        q = torch.randn(2, 2, 5, 8, requires_grad=True)
+        out = F.scaled_dot_product_attention(q, q, q)
+        seen["fn"] = F.scaled_dot_product_attention
+        seen["grad_fn"] = type(out.grad_fn).__name__
+
+    class Spy(TinyNet):
+        def forward(self, batch):
+            t = threading.Thread(target=other_thread)
+            t.start()
+            t.join()
+            seen["main_sdpa"] = F.scaled_dot_product_attention
+            return super().forward(batch)
+
+    models = [Spy() for _ in range(2)]
+    ra = ReplicaArena(models)
+    ra.zero_grad()
+    BatchedForward(models, ra)([d[0] for d in _batches(2, 1, seed=5)])
+    assert seen["fn"] is torch._C._nn.scaled_dot_product_attention
+    assert seen["main_sdpa"] is torch._C._nn.scaled_dot_product_attention
+    assert "Folded" not in seen["grad_fn"], seen["grad_fn"]
+    assert ra.grad_set.abs().sum() > 0
+
+
+def test_batched_forward_unfoldable_attention_is_exact():
+    """k / v broadcast over SDPA's batch (a leading 1) cannot be folded into the
+    node dim: the batched forward takes the math backend and still matches the
+    per-node loop."""
+    from gym_amd.arena import ReplicaArena
+    from gym_amd.replica import BatchedForward
+
+    class Bcast(TinyNet):
+        def forward(self, batch):
+            x, y = batch
+            B, T, _ = x.shape
+            h = self.lin(x)
+            h = self.bn(h.transpose(1, 2)).transpose(1, 2)
+            q, k, v = (t.reshape(B, T, 2, 8).transpose(1, 2) for t in self.qkv(h).split(16, dim=-1))
+            z = F.scaled_dot_product_attention(q, k[:1], v[:1])  # k, v broadcast over the batch
+            h = h + z.transpose(1, 2).reshape(B, T, 16)
+            return F.cross_entropy(self.head(h.mean(1)), y)
+
+    K = 2
+    models = [Bcast() for _ in range(K)]
+    with torch.no_grad():
+        for k, m in enumerate(models):
+            for p in m.parameters():
+                p.add_(0.05 * k * torch.randn_like(p))
+    ra = ReplicaArena(models)
+    data = _batches(K, 1, seed=9)
+    b0 = _bufs(models)
+    ra.zero_grad()
+    for k, m in enumerate(models):
+        m(data[k][0]).backward()
+    ra.sync_grads()
+    g_loop = ra.grad_set.clone()
+    with torch.no_grad():
+        for m, bs in zip(models, b0):
+            for b, v in zip(m.buffers(), bs):
+                b.copy_(v)
+    ra.zero_grad()
+    BatchedForward(models, ra)([data[k][0] for k in range(K)])
+    ra.sync_grads()
+    np.testing.assert_allclose(ra.grad_set.numpy(), g_loop.numpy(), rtol=1e-5, atol=1e-7)
+
+
+def test_batched_forward_follows_the_models_mode():
+    """A model put in eval() after the batched forward was built runs its
+    BatchNorm on running statistics in the vmap path too (as the loop does)."""
+    from gym_amd.arena import ReplicaArena
+    from gym_amd.replica import BatchedForward
+    K = 2
+    models = [TinyNet() for _ in range(K)]
+    ra = ReplicaArena(models)
+    bf = BatchedForward(models, ra)
+    for m in models:
+        m.eval()
+    data = _batches(K, 1, seed=4)
+    b0 = _bufs(models)
+    ra.zero_grad()
+    for k, m in enumerate(models):
+        m(data[k][0]).backward()
+    ra.sync_grads()
+    g_loop = ra.grad_set.clone()
+    ra.zero_grad()
+    bf([data[k][0] for k in range(K)])
+    ra.sync_grads()
+    assert not bf.meta.training
+    np.testing.assert_allclose(ra.grad_set.numpy(), g_loop.numpy(), rtol=1e-5, atol=1e-7)
+    for bs_v, bs_0 in zip(_bufs(models), b0):  # eval: running statistics untouched
+        for v, w in zip(bs_v, bs_0):
+            assert torch.equal(v, w)
