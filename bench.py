@@ -71,13 +71,16 @@ XGMI_LINK_GBS = 153.0      # per xGMI link (SURVEY §8(d) roofline model)
 def setup_dist(gpus):
     if gpus > 1 or "RANK" in os.environ:
         local = int(os.environ.get("LOCAL_RANK", 0))
+        from gym_amd.placement import note_devices
         if os.environ.get("GA_BENCH_BACKEND") == "gloo":
             # rehearsal of the multi-rank path on a 1-GPU box: ranks share the GPUs over gloo
             torch.cuda.set_device(local % torch.cuda.device_count())
             dist.init_process_group("gloo")
+            note_devices()
             return Collective()
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        note_devices()
         if os.environ.get("GA_BENCH_FORCE_EXCHANGE") == "1":
             # rehearsal of the multi-GPU code paths on one GPU: a world-1 RCCL group whose
             # collectives are issued anyway (tests/test_gpu_rccl.py); not a measurement
@@ -1036,7 +1039,7 @@ def main():
         "config": {"workload": f"DiLoCo outer step (configs[2]), {args.model}, {K_total} simulated nodes in total, "
                                f"{args.replicas} per GPU ({'a batched-replica arena, ' if args.replicas > 1 else ''}"
                                f"fused average+pseudo-grad+Nesterov SGD(lr=0.7, mu=0.9)"
-                               f"{', RCCL reduce-scatter/all-gather across GPUs' if coll.world > 1 else ''})",
+                               f"{(', RCCL reduce-scatter/all-gather' if coll.rccl else f', {coll.backend} all-reduce') + ' across GPUs' if coll.world > 1 else ''})",
                    "model": args.model, "nodes_per_gpu": args.replicas, "nodes_total": K_total,
                    "n_params": head["n_params"], "parallelism": f"dp{K_total} (simulated nodes)"},
         "roofline": head["roofline"],

@@ -176,6 +176,8 @@ class MeanReduce:
                 or 4 * ld < SHARD_MIN_BYTES or self.n % 4 or ld % 4 or REPLICA_PLACEMENT_CANDIDATES < 2):
             return reps
 
+        watch = placement.Stopwatch()
+
         def as_set(buf):
             return buf.tensor()[:K * ld].view(K, ld)
 
@@ -195,6 +197,7 @@ class MeanReduce:
         self.placement = {"candidates": len(times), "probe_ms": [round(t, 4) for t in times], "chosen": best,
                           "how": "the caller's replica set moved to the fastest of fresh [K, ld] allocations; "
                                  "candidate 0 = where it was"}
+        watch.stamp(self.placement)
         return reps
 
     def __call__(self, reps):
@@ -321,6 +324,7 @@ class DiLoCoOuter:
                 or reps.stride(1) != 1 or reps.stride(0) % 4 or per % 4):
             return reps
         rep_rec = None
+        watch = placement.Stopwatch()
         if self.relocate_replicas is not None and REPLICA_PLACEMENT_CANDIDATES >= 2 and reps.is_contiguous():
             reps, rep_rec = self._place_replicas(reps, per)
             self._placed_for = (reps.data_ptr(), reps.stride(0))
@@ -344,6 +348,7 @@ class DiLoCoOuter:
                                  "access pattern; candidate 0 = the ordinary allocation"}
         if rep_rec is not None:
             self.placement["replica_set"] = rep_rec
+        watch.stamp(self.placement)  # both stages
         return reps
 
     def _place_replicas(self, reps, per):
@@ -593,6 +598,7 @@ def place_demo_step(encode, decode, P, G, D):
     def run(g, p, d):
         encode(p, g, d)
         decode(p, g)
+    watch = placement.Stopwatch()
     try:  # only the snapshots can run out of memory before anything is touched (candidates: choose)
         (bg, bp, bd), (g2, p2, d2), stages = placement.place_each([G, P, D], run, DEMO_PLACEMENT_CANDIDATES,
                                                                   DEMO_PLACEMENT_MAX_FRAC)
@@ -604,7 +610,7 @@ def place_demo_step(encode, decode, P, G, D):
            "ordinary_ms": round(stages[0], 4), "grad_placed_ms": round(stages[1], 4),
            "param_placed_ms": round(stages[2], 4), "delta_placed_ms": round(stages[3], 4),
            "placed": [b is not None for b in (bg, bp, bd)], "candidates_per_buffer": DEMO_PLACEMENT_CANDIDATES}
-    return (bp, bg, bd), (p2, g2, d2), rec
+    return (bp, bg, bd), (p2, g2, d2), watch.stamp(rec)
 
 
 def demo_codec(coll: Collective, K_local, layout, device, chunk=64, topk=32, bf16_transform="fp32"):

@@ -18,6 +18,7 @@ state buffers, so state_dict() has torch's layout, and load_state_dict()
 moments into those buffers, so a resumed run continues where it stopped.
 """
 import math
+import time
 
 import torch
 
@@ -30,8 +31,12 @@ PLACEMENT_CANDIDATES = 48
 PLACEMENT_MAX_FRAC = 0.3
 PLACEMENT_MIN_BYTES = 32 << 20
 # K > 1 replicas: each replica's moments are placed on their own (probed against that
-# replica's parameter / gradient rows), with fewer candidates per replica
+# replica's parameter / gradient rows), with fewer candidates per replica and a budget:
+# a replica's search stops after ROW_PATIENCE candidates unless the best beats its
+# ordinary rows by > 2%, and the whole search stops at PLACEMENT_ROW_BUDGET_S
 PLACEMENT_ROW_CANDIDATES = 16
+PLACEMENT_ROW_PATIENCE = 3
+PLACEMENT_ROW_BUDGET_S = 0.25
 
 
 def fusable(spec_cls, kwargs, arena):
@@ -53,38 +58,46 @@ def fusable(spec_cls, kwargs, arena):
     return not isinstance(lr, torch.Tensor)
 
 
-def place_moment_rows(P, G, Mr, Vr, max_candidates=None, max_frac=None):
+def place_moment_rows(P, G, Mr, Vr, max_candidates=None, max_frac=None, patience=None, budget_s=None):
     """Per-replica placement of Adam moments (ArenaAdam, K > 1): for each
-    replica k, up to max_candidates fresh allocations of its two moment rows
-    are timed with ga_probe_adam_placement against P[k], G[k] (values
-    unchanged) beside Mr[k], Vr[k] where they are; the fastest keeps them.
-    Returns (new rows M, new rows V -- candidate views or copies of the old
-    rows --, per replica the chosen buffer or None, the record)."""
+    replica k, fresh allocations of its two moment rows are timed with
+    ga_probe_adam_placement against P[k], G[k] (values unchanged) beside Mr[k],
+    Vr[k] where they are; the fastest keeps them.  Budget: up to max_candidates
+    per replica, stopping after `patience` unless the best beats the rows' own
+    time by > 2% (placement.choose), and the whole search ends by budget_s (each
+    replica gets an equal share of what is left).  Rows not moved stay where
+    they were probed (views of the caller's buffers).  Returns (new rows M, new
+    rows V, per replica the chosen buffer or None, the record)."""
     from . import placement
     max_candidates = PLACEMENT_ROW_CANDIDATES if max_candidates is None else max_candidates
     max_frac = PLACEMENT_MAX_FRAC if max_frac is None else max_frac
+    patience = PLACEMENT_ROW_PATIENCE if patience is None else patience
+    budget_s = PLACEMENT_ROW_BUDGET_S if budget_s is None else budget_s
+    watch = placement.Stopwatch()
+    t_end = watch.t0 + budget_s
     K, ld = P.shape[0], Mr[0].numel()
     bufs, probe_ms, chosen = [], [], []
     for k in range(K):
         Pk, Gk = P[k, :ld], G[k, :ld]
 
         def probe(M, V):
-            return placement.time_probe(lambda: ops.probe_adam_placement(Pk, Gk, M, V))
+            return placement.time_probe(lambda: ops.probe_adam_placement(Pk, Gk, M, V), reps=2)
 
         def split(buf):
             t = buf.tensor()
             return t[:ld], t[ld:2 * ld]
 
+        now = time.perf_counter()
+        deadline = now + max(0.0, t_end - now) / (K - k)
         best, times = placement.choose(2 * ld * 4, P.device, lambda b: probe(*split(b)), probe(Mr[k], Vr[k]),
-                                       max_candidates, max_frac)
+                                       max_candidates, max_frac, patience=patience, deadline=deadline)
         bufs.append(best)
         probe_ms.append([round(t, 4) for t in times])
         chosen.append(min(range(len(times)), key=lambda i: times[i]) if best is not None else 0)
     outM, outV = [], []
-    any_placed = any(b is not None for b in bufs)
     for k, b in enumerate(bufs):
-        if b is None:  # kept where they are (copies when the [K, ld] pair is released)
-            m, v = (Mr[k].clone(), Vr[k].clone()) if any_placed else (Mr[k], Vr[k])
+        if b is None:  # kept where they were probed
+            m, v = Mr[k], Vr[k]
         else:
             t = b.tensor()
             m, v = t[:ld], t[ld:2 * ld]
@@ -92,11 +105,12 @@ def place_moment_rows(P, G, Mr, Vr, max_candidates=None, max_frac=None):
             v.copy_(Vr[k])
         outM.append(m)
         outV.append(v)
-    rec = {"per_replica": True, "candidates_per_replica": max_candidates, "chosen": chosen,
+    rec = {"per_replica": True, "candidates_per_replica": max_candidates, "patience": patience,
+           "budget_s": budget_s, "candidates_probed": sum(len(t) - 1 for t in probe_ms), "chosen": chosen,
            "placed_rows": sum(b is not None for b in bufs),
            "probe_ms_ordinary_sum": round(sum(t[0] for t in probe_ms), 4),
            "probe_ms_chosen_sum": round(sum(min(t) for t in probe_ms), 4), "probe_ms": probe_ms}
-    return outM, outV, bufs, rec
+    return outM, outV, bufs, watch.stamp(rec)
 
 
 class ArenaAdam(torch.optim.Optimizer):
@@ -151,6 +165,8 @@ class ArenaAdam(torch.optim.Optimizer):
         self._partials = ops.sumsq_partials(dev, self.K)
         self._clip = torch.ones(2 * self.K, dtype=torch.float32, device=dev)
         self._placed = None  # the candidate buffer holding M and V once _place chose one
+        self._placed_for = None  # (P, G) data pointers the moments were placed against
+        self._placements = 0  # searches run (a relocated P / G set is searched again)
         self.placement = None  # the placement record (probe times, or why it was skipped)
         self.place_opt = placement  # False: never probe / move the moments (gym_amd.placement.policy)
 
@@ -219,8 +235,12 @@ class ArenaAdam(torch.optim.Optimizer):
         rows (the kernel's replica-major grid streams one replica's four rows
         at a time; a [K, ld] candidate at K = 32 x 124M would be 32 GB, so the
         memory budget would leave no choice); the step then runs one launch
-        per replica."""
-        self._place_done = True
+        per replica.  When the parameter / gradient set is later moved (the
+        outer step's own placement relocates the replica set at step H), the
+        search runs again against the new rows, so the moments' placement
+        always describes the step that runs."""
+        self._placed_for = (self.P.data_ptr(), self.G.data_ptr())
+        self._placements += 1
         nb = 2 * self.K * self.ld * 4
         if (self.P.device.type != "cuda" or nb < PLACEMENT_MIN_BYTES or PLACEMENT_CANDIDATES < 2
                 or self.ld % 4 or self.P.stride(-1) != 1):
@@ -230,10 +250,13 @@ class ArenaAdam(torch.optim.Optimizer):
         if not ok:
             self.placement = {"placed": False, "why": why}
             return
+        watch = placement.Stopwatch()
         if self.K == 1:
             self._place_whole(placement, nb)
         else:
             self._place_rows(placement)
+        watch.stamp(self.placement)
+        self.placement["searches"] = self._placements
 
     def _place_whole(self, placement, nb):
         KL = self.K * self.ld
@@ -294,7 +317,7 @@ class ArenaAdam(torch.optim.Optimizer):
         ranges = [self._ranges(k) for k in range(self.K)]
         for ar in self.arenas:
             ar.sync_grads()
-        if not getattr(self, "_place_done", False):
+        if self._placed_for != (self.P.data_ptr(), self.G.data_ptr()):
             self._place()
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = float(g["lr"]), g["betas"], float(g["eps"]), float(g["weight_decay"])

@@ -37,19 +37,61 @@ seen corrupted on this stack when interleaved with ordinary allocations
 This module only moves memory; every kernel stays behind the C ABI.
 """
 import os
+import socket
+import time
 
 import torch
 import torch.distributed as dist
 
 
+_VISIBLE_ENVS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+_SHARING = None  # (process group, shared?) recorded by note_devices() for that group
+
+
+def device_identity():
+    """This process's GPU as the machine knows it: host, UUID and PCI location
+    (the same physical card gives the same string in every process, whatever
+    its visible-devices numbering)."""
+    host = socket.gethostname()
+    if not torch.cuda.is_available():
+        return f"{host}|cpu"
+    p = torch.cuda.get_device_properties(torch.cuda.current_device())
+    pci = tuple(getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    return f"{host}|{getattr(p, 'uuid', None)}|{pci}"
+
+
+def note_devices(group=None):
+    """Collective, once per process group right after init_process_group (the
+    trainer's and the bench's setup do it): every rank's device_identity() is
+    gathered and this rank records whether another rank of the group drives the
+    same physical GPU.  Returns that answer (None without a process group)."""
+    global _SHARING
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    group = group or dist.group.WORLD
+    ids = [None] * dist.get_world_size(group)
+    mine = device_identity()
+    dist.all_gather_object(ids, mine, group=group)
+    _SHARING = (group, ids.count(mine) > 1)
+    return _SHARING[1]
+
+
 def device_shared():
-    """True when this process shares its GPU with other ranks of the job (more
-    ranks in the default process group than visible devices: the reference's
-    nodes-over-gloo-on-one-card layout)."""
+    """True when this process shares its GPU with other ranks of the job.  After
+    note_devices(): by device identity.  Otherwise a heuristic: more ranks on
+    this host (LOCAL_WORLD_SIZE) than visible devices -- the reference's
+    nodes-over-gloo-on-one-card layout -- except under a launcher that pins one
+    GPU per rank through a visible-devices variable (one device visible), which
+    it cannot tell apart without the exchange and so does not call shared."""
     if not (dist.is_available() and dist.is_initialized()):
         return False
+    if _SHARING is not None and _SHARING[0] is dist.group.WORLD:
+        return _SHARING[1]
     local = int(os.environ.get("LOCAL_WORLD_SIZE", dist.get_world_size()))
-    return local > max(1, torch.cuda.device_count())
+    count = max(1, torch.cuda.device_count())
+    if count == 1 and any(os.environ.get(v) for v in _VISIBLE_ENVS):
+        return False
+    return local > count
 
 
 def policy(requested=True):
@@ -83,6 +125,18 @@ class DeviceBuffer:
         self._t = None
 
 
+class Stopwatch:
+    """Wall time of one owner's placement search (its record's "search_s")."""
+
+    def __init__(self):
+        self.t0 = time.perf_counter()
+
+    def stamp(self, record):
+        if record is not None:
+            record["search_s"] = round(time.perf_counter() - self.t0, 3)
+        return record
+
+
 def time_probe(fn, reps=3):
     """ms per call of fn (one warm-up, then reps calls between two events)."""
     fn()
@@ -95,7 +149,8 @@ def time_probe(fn, reps=3):
     return e0.elapsed_time(e1) / reps
 
 
-def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=DeviceBuffer):
+def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=DeviceBuffer, patience=None,
+           min_gain=0.02, deadline=None):
     """Create up to max_candidates - 1 allocations of nbytes one at a time (all
     held until the choice is made, so each is distinct memory), time
     probe(buffer) on each, and return (the fastest buffer, or None when none
@@ -103,7 +158,13 @@ def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=De
     order with the baseline first).  At most max_frac of the free device memory
     is taken; an allocation failure (OutOfMemoryError) ends the search with what
     was probed.  Any other error -- a rejected or faulting probe launch -- is
-    raised: the search must not hide a poisoned context."""
+    raised: the search must not hide a poisoned context.
+
+    Budget: with `patience`, the search stops after that many candidates unless
+    the best so far beats baseline_ms by more than min_gain (the caller's memory
+    is then already in a fast class, and more candidates would only cost time);
+    with `deadline` (a time.perf_counter() value) no candidate is created after
+    it.  The best candidate found is kept either way."""
     dev = torch.device(device)
     torch.cuda.empty_cache()  # fresh blocks, not cached free memory
     times = [baseline_ms]
@@ -111,6 +172,10 @@ def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=De
     budget = max_frac * torch.cuda.mem_get_info(dev)[0]
     try:
         while len(times) < max_candidates and (len(held) + 1) * nbytes <= budget:
+            if deadline is not None and time.perf_counter() >= deadline:
+                break
+            if patience is not None and len(held) >= patience and best_t >= baseline_ms * (1.0 - min_gain):
+                break
             try:
                 buf = kind(nbytes, dev)
             except torch.cuda.OutOfMemoryError:
@@ -127,7 +192,6 @@ def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=De
         held = None
         torch.cuda.empty_cache()
     return best, times
-
 
 
 def place_each(tensors, run, max_candidates, max_frac, reps=3):

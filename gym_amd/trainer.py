@@ -235,3 +235,5 @@ class LocalTrainer(Trainer):
         kw = {"device_id": torch.device(f"cuda:{gpu}")} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=self.rank, world_size=world, **kw)
         self.device = torch.device(f"cuda:{gpu}")
+        from .placement import note_devices
+        note_devices()  # placement is skipped on a GPU other ranks of the job share

@@ -106,3 +106,72 @@ def test_replica_arena_relocate_grads():
     assert (new == 0).all() and all(lo <= p.grad.data_ptr() < hi for p in ra.params)
     ra.sync_grads()
     assert all(lo <= p.grad.data_ptr() < hi for p in ra.params)
+
+
+def test_device_sharing_by_identity(monkeypatch, tmp_path):
+    """note_devices(): sharing decided by the physical GPU's identity, not by
+    counting ranks against visible devices; a per-rank pinning launcher (one
+    visible device, HIP_VISIBLE_DEVICES set) is not taken for sharing by the
+    fallback rule either."""
+    monkeypatch.delenv("GA_PLACEMENT", raising=False)
+    for v in placement._VISIBLE_ENVS:
+        monkeypatch.delenv(v, raising=False)
+    dist.init_process_group("gloo", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+        monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+        assert placement.device_shared()  # fallback rule: 4 ranks, 1 device
+        monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")  # pinned per rank by the launcher
+        assert not placement.device_shared()
+        monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+        assert placement.note_devices() is False  # one rank: nobody shares its GPU
+        assert not placement.device_shared()  # the identity answer wins over the count
+        ids = iter(["h|gpu0"])
+        monkeypatch.setattr(placement, "device_identity", lambda: next(ids, "h|gpu0"))
+        monkeypatch.setattr(dist, "all_gather_object", lambda out, obj, group=None: out.__setitem__(
+            slice(None), [obj, "h|gpu0", "h|gpu1"]))
+        assert placement.note_devices() is True  # another rank drives the same card
+        assert placement.policy(True) == (False, "GPU shared by several processes of the job")
+    finally:
+        dist.destroy_process_group()
+        placement._SHARING = None
+    assert not placement.device_shared()  # no process group
+
+
+class _FakeBuf:
+    made = 0
+
+    def __init__(self, nbytes, dev):
+        _FakeBuf.made += 1
+        self.i = _FakeBuf.made
+
+    def release(self):
+        pass
+
+
+def _choose(monkeypatch, times, **kw):
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: None)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (1 << 40, 1 << 40))
+    _FakeBuf.made = 0
+    t = iter(times)
+    return placement.choose(1 << 20, "cpu", lambda b: next(t), 1.0, 16, 0.3, kind=_FakeBuf, **kw)
+
+
+def test_choose_budget(monkeypatch):
+    """placement.choose's budget: with patience p the search stops after p
+    candidates unless the best beats the baseline by > min_gain; a deadline
+    in the past creates no candidate; the best found is kept either way."""
+    best, times = _choose(monkeypatch, [0.995, 1.01, 0.99] + [0.5] * 20, patience=3)
+    assert len(times) == 4 and best.i == 3  # three probed, 1% gain < 2%: stop, keep the best
+    best, times = _choose(monkeypatch, [1.1, 0.9, 1.2, 0.95, 0.85] + [2.0] * 20, patience=3)
+    assert len(times) == 16 and best.i == 5  # 10% gain: the search runs to max_candidates
+    best, times = _choose(monkeypatch, [0.5] * 20, deadline=0.0)
+    assert best is None and times == [1.0]
+    best, times = _choose(monkeypatch, [1.0 + i / 100 for i in range(20)])
+    assert best is None and len(times) == 16  # no budget: every candidate, none faster
+
+
+def test_stopwatch_stamps_search_time():
+    rec = placement.Stopwatch().stamp({"chosen": 0})
+    assert rec["search_s"] >= 0.0
+    assert placement.Stopwatch().stamp(None) is None
