@@ -1019,10 +1019,14 @@ __global__ __launch_bounds__(kDmBlock, sizeof(CntT) == 1 ? 4 : 3) void demo_deco
             // scatter-mean (demo.py:331-352): sources in node order; one source's
             // indices are distinct, so each source is one conflict-free pass and the
             // per-coefficient sums accumulate in node order.
+            // REF: the running sum rounded to bf16 after every source's add, in node order
+            // (torch's bf16 scatter_reduce adds with bf16 rounding per add; its GPU atomics
+            // add in an unspecified order, which matters only at 3+ hitters of a position)
             auto hit = [&](int x, float v) {
                 if (x >= 0 && x < nvalid) {
                     const int b = x / n2, dd = x - b * n2;
-                    S[b * kLd + dd] += v;
+                    const float sum = S[b * kLd + dd] + v;
+                    S[b * kLd + dd] = REF ? bf16r(sum) : sum;
                     cnt[b * 64 + dd] += 1;
                 }
             };

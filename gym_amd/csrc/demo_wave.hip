@@ -135,6 +135,15 @@ __device__ __forceinline__ int find_tensor(const ga_demo_tensor* __restrict__ T,
     return lo;
 }
 
+// The decode's second half of waves (w >= 4: the partner of wave w - 4 on its SIMD,
+// the arbitration loser by age) runs at static priority 1: the 8-source decode at
+// 350M 1.113 -> 1.058 ms in one process (profiles/r06e_ab_demo_wave_sched.txt;
+// MI355X_MICROARCH.md, two waves per SIMD, item 4).  The encode measured no gain
+// from it, nor from a start stagger of the second half (both kernels).
+__device__ __forceinline__ void decode_wave_priority(int wid) {
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+}
+
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int j) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, j);
 }
@@ -452,11 +461,11 @@ __device__ __forceinline__ void chunk64_tail(const f32x16 (&Y)[2][2], int k, T* 
     W.bm[2 * lane] = 0u;
     W.bm[2 * lane + 1] = 0u;
     if (C <= kCand) {
-        // compact the candidates: (pos, bits) at the lane's next slot, others to its discard slot
-        int at = excl;
         uint2* L2 = reinterpret_cast<uint2*>(W.lst);
         float T0c = T0f;  // an opaque copy: the 64 compares are redone here, not kept as 64 lane masks
         asm volatile("" : "+v"(T0c));
+        // compact the candidates: (pos, bits) at the lane's next slot, others to its discard slot
+        int at = excl;
 #pragma unroll
         for (int par = 0; par < 2; ++par)
 #pragma unroll
@@ -1428,6 +1437,7 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     __syncthreads();
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     DecLDS& W = wl[wid];
+    decode_wave_priority(wid);
     const int64_t total = (int64_t)nchunks + ngroups;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int tix = -1;

@@ -46,7 +46,11 @@ extern "C" {
  * bf16-representable values), every stage of each transform rounded to bf16 in
  * the reference's contraction order (chunk rows first), the delta rounded after
  * the decay and after the gradient add (exogym/strategy/demo_impl/demo.py:
- * 159-180, 235-252 as torch runs it). */
+ * 159-180, 235-252 as torch runs it); the decode's scatter-mean adds the sources
+ * in node order with the sum rounded to bf16 after every add, then divides
+ * (demo.py:339-341: torch's bf16 scatter_reduce; on the GPU its atomic adds run
+ * in an unspecified order, so at 3+ hitters of one position node order is one
+ * of the orders the reference can produce). */
 #define GA_BF16_REF 2
 
 /* replica-set layouts (SPARTA entry points):

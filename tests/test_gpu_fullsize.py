@@ -413,6 +413,43 @@ def test_replica_loop_placements_bit_exact_under_allocation_churn():
             assert torch.equal(x, y)
 
 
+def test_adam_moments_searched_again_after_relocation():
+    """ArenaAdam at K > 1 places each replica's moment rows against that
+    replica's parameter / gradient rows; when the parameter set moves (the
+    outer step's relocation at step H), the next step searches again, so the
+    record describes the rows the step streams with.  The budget holds (the
+    record's search_s), and the trajectory is bit-identical to placement off."""
+    from gym_amd import fused_optim as F
+    from gym_amd.arena import ReplicaArena
+    from gym_amd.fused_optim import ArenaAdam
+    torch.manual_seed(0)
+    base = torch.nn.Sequential(*[torch.nn.Linear(2048, 2048) for _ in range(3)]).to(DEV)
+
+    def run(placed):
+        ra = ReplicaArena([copy.deepcopy(base) for _ in range(4)])
+        opt = ArenaAdam(ra.params, ra, lr=1e-3, weight_decay=0.01, placement=placed)
+        g = torch.Generator(device=DEV)
+        g.manual_seed(5)
+        recs = []
+        for step in range(4):
+            if step == 2:
+                ra.relocate_params(ra.flat_set.clone())  # as DiLoCoOuter._place_replicas does
+            for p in ra.params:
+                p.grad = torch.randn(p.shape, device=DEV, generator=g) * 1e-2
+            opt.step()
+            recs.append(dict(opt.placement or {}))
+        return ra.flat_set.clone(), opt.M.clone(), opt.V.clone(), recs
+    a = run(True)
+    b = run(False)
+    for x, y in zip(a[:3], b[:3]):
+        assert torch.equal(x, y)
+    recs = a[3]
+    assert recs[0]["searches"] == 1 and recs[2]["searches"] == 2 and recs[3]["searches"] == 2
+    for r in (recs[0], recs[2]):
+        assert r["per_replica"] and len(r["probe_ms"]) == 4
+        assert r["search_s"] < F.PLACEMENT_ROW_BUDGET_S + 1.0, r["search_s"]
+
+
 def test_demo_step_placement_leaves_the_step_unchanged():
     """The DeMo optimizer moves its gradient, parameter and delta arenas into the
     device allocations its step runs fastest on, once, after the first step
