@@ -135,13 +135,14 @@ __device__ __forceinline__ int find_tensor(const ga_demo_tensor* __restrict__ T,
     return lo;
 }
 
-// The decode's second half of waves (w >= 4: the partner of wave w - 4 on its SIMD,
-// the arbitration loser by age) runs at static priority 1: the 8-source decode at
-// 350M 1.113 -> 1.058 ms in one process (profiles/r06e_ab_demo_wave_sched.txt;
+// The several-source decode's second half of waves (w >= 4: the partner of wave
+// w - 4 on its SIMD, the arbitration loser by age) runs at static priority 1: at
+// 350M in one process 8 sources 1.003 -> 0.958 ms, 2 sources 0.825 -> 0.817 ms, but
+// one source 0.811 -> 0.844 ms, so only for S >= 2 (profiles/r06f_ab_demo_decode_prio.txt;
 // MI355X_MICROARCH.md, two waves per SIMD, item 4).  The encode measured no gain
-// from it, nor from a start stagger of the second half (both kernels).
-__device__ __forceinline__ void decode_wave_priority(int wid) {
-    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+// from it, nor from a start stagger of the second half (profiles/r06e_ab_demo_wave_sched.txt).
+__device__ __forceinline__ void decode_wave_priority(int wid, int S) {
+    if (S >= 2 && wid >= 4) __builtin_amdgcn_s_setprio(1);
 }
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int j) {
@@ -1437,7 +1438,7 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     __syncthreads();
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     DecLDS& W = wl[wid];
-    decode_wave_priority(wid);
+    decode_wave_priority(wid, S);
     const int64_t total = (int64_t)nchunks + ngroups;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int tix = -1;
