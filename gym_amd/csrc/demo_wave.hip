@@ -141,8 +141,11 @@ __device__ __forceinline__ int find_tensor(const ga_demo_tensor* __restrict__ T,
 // one source 0.811 -> 0.844 ms, so only for S >= 2 (profiles/r06f_ab_demo_decode_prio.txt;
 // MI355X_MICROARCH.md, two waves per SIMD, item 4).  The encode measured no gain
 // from it, nor from a start stagger of the second half (profiles/r06e_ab_demo_wave_sched.txt).
-__device__ __forceinline__ void decode_wave_priority(int wid, int S) {
-    if (S >= 2 && wid >= 4) __builtin_amdgcn_s_setprio(1);
+// (one asm statement holding its own scalar branch: a branch in the kernel's control
+// flow here made the register allocator spill 124 B/lane in the chunk loop)
+__device__ __forceinline__ void decode_wave_priority() {
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    asm volatile("s_cmp_lt_u32 %0, 4\n\ts_cbranch_scc1 1f\n\ts_setprio 1\n1:" ::"s"(w) : "scc");
 }
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int j) {
@@ -1157,27 +1160,46 @@ __device__ __forceinline__ void apply_signs(const float4* tile, T* param, T* gra
         }
         return;
     }
-    for (int64_t r = 0; r < K; ++r) {  // a partial row group
+    for (int64_t r = 0; r < K; ++r) {  // a partial row group: 8 row quads' loads, then their stores
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if ((lane >> 4) + 4 * i >= nrows) continue;
-            const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
-            const float sg[4] = {v.x, v.y, v.z, v.w};
-            T* a = at_off(param + r * ld, coal_off(i, lane, stride));
+        for (int i0 = 0; i0 < 16; i0 += 8) {
+            float f[8][4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) Elem<T>::store(a + e, fmaf(-lr, sg[e], Elem<T>::load(a + e)));
-            if (grad) {
-                T* gq = at_off(grad + r * ld, coal_off(i, lane, stride));
+            for (int i = 0; i < 8; ++i) {
+                const bool live = (lane >> 4) + 4 * (i0 + i) < nrows;
+                const T* a = at_off(param + r * ld, coal_off(i0 + i, lane, stride));
 #pragma unroll
-                for (int e = 0; e < 4; ++e) Elem<T>::store(gq + e, sg[e]);
+                for (int e = 0; e < 4; ++e) f[i][e] = live ? Elem<T>::load(a + e) : 0.f;
+            }
+#pragma unroll
+            for (int ii = 0; ii < 8; ++ii) {
+                const int i = i0 + ii;
+                if ((lane >> 4) + 4 * i >= nrows) continue;
+                const float4 v = tile[t4((lane >> 4) + 4 * i, lane & 15)];
+                const float sg[4] = {v.x, v.y, v.z, v.w};
+                T* a = at_off(param + r * ld, coal_off(i, lane, stride));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Elem<T>::store(a + e, fmaf(-lr, sg[e], f[ii][e]));
+                if (grad) {
+                    T* gq = at_off(grad + r * ld, coal_off(i, lane, stride));
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) Elem<T>::store(gq + e, sg[e]);
+                }
             }
         }
     }
 }
 
 // node-ordered scatter-add of S sources' entries (n per source, entry j -> tile row
-// row_of(j)) and the 4-bit hit counts; sources in order, one source per pass (a
-// source's indices are distinct, so the adds of one pass never collide)
+// row_of(j)) and the 4-bit hit counts, sources in order (a source's indices are
+// distinct, so its adds never collide; one wave's LDS adds run in issue order, so
+// the per-coefficient sums accumulate in node order).  A row group holds up to
+// 64 x k entries per source: each lane loads kGrpBatch of them before any add, so
+// the scatter costs one memory latency per batch instead of one per entry (S x 32
+// dependent round trips per row group at k = 32, which made the row groups the
+// decode's tail)
+constexpr int kGrpBatch = 16;
+
 template <typename RowOf>
 __device__ __forceinline__ void scatter_sources(DecLDS& W, const int32_t* __restrict__ payload, int64_t pstride,
                                                 int64_t M, int64_t e0, int S, int n, int nvalid, RowOf row_of,
@@ -1185,14 +1207,25 @@ __device__ __forceinline__ void scatter_sources(DecLDS& W, const int32_t* __rest
     for (int s = 0; s < S; ++s) {
         const int32_t* pi = payload + (int64_t)s * pstride + e0;
         const float* pv = reinterpret_cast<const float*>(payload + (int64_t)s * pstride + M) + e0;
-        for (int j = lane; j < n; j += 64) {
-            const int x = pi[j];
-            const float v = pv[j];
-            if ((unsigned)x < (unsigned)nvalid) {
-                const int row = row_of(j, x), col = nvalid == 64 ? x : (x & 63);
-                atomicAdd(&W.tile[fidx(row, col)], v);
-                const int cid = row * 64 + col;
-                atomicAdd(&W.aux[cid >> 3], 1u << (4 * (cid & 7)));
+        for (int j0 = 0; j0 < n; j0 += 64 * kGrpBatch) {
+            int xb[kGrpBatch];
+            float vb[kGrpBatch];
+#pragma unroll
+            for (int u = 0; u < kGrpBatch; ++u) {
+                const int j = j0 + 64 * u + lane;
+                xb[u] = j < n ? pi[j] : -1;
+                vb[u] = j < n ? pv[j] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kGrpBatch; ++u) {
+                const int x = xb[u];
+                if ((unsigned)x < (unsigned)nvalid) {
+                    const int j = j0 + 64 * u + lane;
+                    const int row = row_of(j, x), col = nvalid == 64 ? x : (x & 63);
+                    atomicAdd(&W.tile[fidx(row, col)], vb[u]);
+                    const int cid = row * 64 + col;
+                    atomicAdd(&W.aux[cid >> 3], 1u << (4 * (cid & 7)));
+                }
             }
         }
         WAVE_LDS_SYNC();
@@ -1379,8 +1412,6 @@ __device__ __forceinline__ void dgroup(const ga_demo_rowgroup& rg, const int32_t
     const bool vec = ptr_vec && (rg.offset % 4 == 0);
     float4* tile = reinterpret_cast<float4*>(W.tile);
     const int lane = lane_id(), l = lane & 31, h = lane >> 5;
-    PRaw<T> pre;  // a full group's replica 0, in flight behind the transform
-    if (rows == 64) load_coal_raw(param + rg.offset, 64, vec, lane, pre);
 #pragma unroll
     for (int i = 0; i < 16; ++i) tile[i * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     reinterpret_cast<uint4*>(W.aux)[lane] = make_uint4(0u, 0u, 0u, 0u);
@@ -1396,6 +1427,9 @@ __device__ __forceinline__ void dgroup(const ga_demo_rowgroup& rg, const int32_t
         }
         WAVE_LDS_SYNC();
     }
+    PRaw<T> pre;  // a full group's replica 0, in flight behind the transform (after the scatter,
+                  // whose double-buffered entry batches need the registers)
+    if (rows == 64) load_coal_raw(param + rg.offset, 64, vec, lane, pre);
     // R^T[c][row] = sum_d F[c][d] X[row][d] for rows l (s = 0) and 63 - l (s = 1)
     const int c0 = pi_col(0, l), c1 = pi_col(1, l);
     f32x16 r[2][2];
@@ -1434,11 +1468,11 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     int S, T* param, T* grad, int64_t K, int64_t ld, float lr, int ptr_vec) {
     __shared__ float Hb[32 * kLd];
     __shared__ DecLDS wl[kWaves];
+    if constexpr (NTS) decode_wave_priority();  // NTS: the launch's S >= 2 instantiation
     for (int q = threadIdx.x; q < 32 * 64; q += kThreads) Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
     __syncthreads();
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     DecLDS& W = wl[wid];
-    decode_wave_priority(wid, S);
     const int64_t total = (int64_t)nchunks + ngroups;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int tix = -1;
