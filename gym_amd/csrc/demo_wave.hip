@@ -919,7 +919,9 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
     int64_t K, float lr, float decay, float wd_factor, int32_t* payload0, int64_t pstride, int64_t M, int ptr_vec) {
     __shared__ float Hb[32 * kLd];
     __shared__ WaveLDS wl[kWaves];
+    __shared__ int next_job;  // the workgroup's job counter
     for (int q = threadIdx.x; q < 32 * 64; q += kThreads) Hb[(q >> 6) * kLd + (q & 63)] = F64[q];
+    next_job = 0;  // every lane stores the same 0 (no branch)
     __syncthreads();
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);  // wave-uniform: scalar job loop
     WaveLDS& W = wl[wid];
@@ -927,11 +929,35 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
     const int64_t n64 = (int64_t)nchunks * K;
     const int64_t total = n64 + (int64_t)ngroups * K;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
+    // The workgroup owns jobs b*8 + w + r*stride (w < 8), i.e. its index i -> job
+    // b*8 + (i & 7) + (i >> 3) * stride, increasing in i: indices [0, nc) are 64x64
+    // chunks, [nc, nt) row groups (the highest job numbers).  Its 8 waves take indices
+    // from one LDS counter, row groups FIRST: a row group costs about two chunks, and
+    // taken last (as a static assignment does) it was the kernel's tail, the wave that
+    // drew it finishing ~0.03 ms after the rest (profiles/r06o_*); taken first, its
+    // siblings take the chunks it would have had.
+    const int64_t b8 = (int64_t)blockIdx.x * kWaves;
+    auto below = [&](int64_t lim) {  // this workgroup's indices whose job is < lim (32-bit:
+        const uint32_t st = (uint32_t)stride;  // the launch keeps the job space below 2^31)
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w)
+            if (b8 + w < lim) c += ((uint32_t)(lim - (b8 + w)) + st - 1u) / st;
+        return (int64_t)c;
+    };
+    const int64_t nc = below(n64), nt = below(total), ng = nt - nc;
     int tix = -1;
     int64_t last_rep = -1;
-    int64_t job = (int64_t)blockIdx.x * kWaves + wid;
-    for (; job < n64; job += stride) {  // 64x64 chunks
-        {
+    while (true) {
+        // lane 0 draws (an LDS atomic at any LDS address; ds_append addresses only the
+        // first 64 KB through M0[15:0], and this counter sits past the wave tiles)
+        int tv = 0;
+        if (lane_id() == 0) tv = atomicAdd(&next_job, 1);
+        const int64_t t = __builtin_amdgcn_readfirstlane(tv);
+        if (t >= nt) break;
+        const int64_t i = t < ng ? nc + t : t - ng;
+        const int64_t job = b8 + (i & 7) + (i >> 3) * stride;
+        if (job < n64) {  // a 64x64 chunk
             const int64_t rep = job / nchunks;
             const int chunk = (int)(job - rep * nchunks);
             if (rep != last_rep) {
@@ -950,10 +976,7 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
 #endif
             );
             DW_CNT(9);
-        }
-    }
-    for (; job < total; job += stride) {  // row groups
-        {
+        } else {  // a row group
             const int64_t j = job - n64;
             const int64_t rep = j / ngroups;
             const int g = (int)(j - rep * ngroups);
@@ -1294,9 +1317,12 @@ __device__ __forceinline__ void dchunk_params(const ga_demo_tensor& td, int c, c
     load_coal_raw(param + chunk_base(td, c), td.cols, chunk_vec(td, ptr_vec), lane_id(), p0);
 }
 
-// sign(g) of chunk c into the tile (swizzled row-major) from the entries in `in`
-template <int MS>
-__device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn<MS>& in, const float* Hb, DecLDS& W) {
+// sign(g) of chunk c into the tile (swizzled row-major) from the entries in `in`;
+// `consumed()` runs as soon as the entries are in LDS (the caller loads the next
+// chunk's entries into `in` there, a whole transform ahead of their use)
+template <int MS, typename Consumed>
+__device__ __forceinline__ void dchunk_signs(int k, int S, DecIn<MS>& in, const float* Hb, DecLDS& W,
+                                             Consumed consumed) {
     float4* tile = reinterpret_cast<float4*>(W.tile);
     const int lane = lane_id(), l = lane & 31, h = lane >> 5;
     const int (&xs)[MS] = in.xs;
@@ -1314,6 +1340,7 @@ __device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn<MS>& in, 
         uint2* lstp = reinterpret_cast<uint2*>(W.aux);
         int np0, np1;
         parity_lists(epos, ebits, ent, lane, lstp, np0, np1);
+        consumed();
 #pragma unroll
         for (int H = 0; H < 2; ++H) {
             f32x16 Re, Ro;
@@ -1345,6 +1372,7 @@ __device__ __forceinline__ void dchunk_signs(int k, int S, const DecIn<MS>& in, 
             }
             WAVE_LDS_SYNC();
         }
+        consumed();
         // U = X . F^T: U[b][l] = ue + uo, U[b][63 - l] = ue - uo (even / odd frequency d)
         f32x16 U[2][2];  // [b block][column set]
 #pragma unroll
@@ -1477,9 +1505,10 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int tix = -1;
     int64_t job = (int64_t)blockIdx.x * kWaves + wid;
-    // 64x64 chunks, software-pipelined: chunk j+1's entries are loaded before chunk j's
-    // stores (vmcnt retires in order: a load issued behind the stores would wait for
-    // them) and its parameters right after them, a whole transform ahead of their use
+    // 64x64 chunks, software-pipelined: chunk j+1's entries are loaded as soon as chunk
+    // j's are in LDS (before chunk j's transform and stores: vmcnt retires in order, so a
+    // load issued behind the stores would wait for them) and its parameters right after
+    // chunk j's stores, a whole transform ahead of their use
     if (job < nchunks) {
         DecIn<MS> cur;
         PRaw<T> p0;
@@ -1489,16 +1518,20 @@ __global__ __launch_bounds__(kThreads) void decode_kernel(
         dchunk_params<T>(td, (int)job - td.chunk_start, param, ptr_vec, p0);
         while (true) {
             const int c = (int)job - td.chunk_start;
-            dchunk_signs(td.k, S, cur, Hb, W);
             const int64_t base = chunk_base(td, c);
             const bool vec = chunk_vec(td, ptr_vec);
-            const int cols = td.cols;
+            const int cols = td.cols, kc = td.k;
             job += stride;
             if (job < nchunks) {
                 tix = find_tensor(tens, ntens, tix, (int)job);
                 td = tens[tix];
-                dchunk_entries(td, (int)job - td.chunk_start, payload, pstride, M, S, cur);
             }
+            // the next chunk's entries are issued once this chunk's are in LDS: in flight
+            // behind this chunk's transform and stores (vmcnt retires in order: older than
+            // the stores, so waiting for them never waits for the stores)
+            dchunk_signs(kc, S, cur, Hb, W, [&] {
+                if (job < nchunks) dchunk_entries(td, (int)job - td.chunk_start, payload, pstride, M, S, cur);
+            });
             apply_signs<T, NTS>(reinterpret_cast<const float4*>(W.tile), param + base, grad ? grad + base : nullptr,
                                 K, ld, cols, vec, 64, lr, lane_id(), p0);
             WAVE_LDS_SYNC();
@@ -1576,7 +1609,7 @@ extern "C" GA_API int ga_demo_encode_sym(int dtype, const ga_demo_tensor* tensor
     GA_REQUIRE(nchunks == 0 || (tensors && ntensors >= 1), "ga_demo_encode_sym: no descriptors");
     GA_REQUIRE(ngroups == 0 || groups, "ga_demo_encode_sym: no row groups");
     GA_REQUIRE(F64 && param && grad && delta && payload, "ga_demo_encode_sym: null buffer");
-    GA_REQUIRE(K >= 1 && ((int64_t)nchunks + ngroups) * K < (1ll << 40), "ga_demo_encode_sym: K=%lld out of range",
+    GA_REQUIRE(K >= 1 && ((int64_t)nchunks + ngroups) * K < (1ll << 31), "ga_demo_encode_sym: K=%lld out of range",
                (long long)K);
     GA_REQUIRE(K == 1 || (ld > 0 && payload_stride >= 2 * M), "ga_demo_encode_sym: bad replica strides");
     const int vb = dtype == GA_F32 ? 16 : 8;
