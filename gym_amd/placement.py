@@ -149,6 +149,11 @@ def time_probe(fn, reps=3):
     return e0.elapsed_time(e1) / reps
 
 
+# wall-time cap of one candidate search when the caller gives no deadline (a box whose
+# large allocations are slow took 4.2 s for AdamW's 48 candidates, profiles/r06q_bench.json)
+SEARCH_BUDGET_S = 1.0
+
+
 def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=DeviceBuffer, patience=None,
            min_gain=0.02, deadline=None):
     """Create up to max_candidates - 1 allocations of nbytes one at a time (all
@@ -163,8 +168,11 @@ def choose(nbytes, device, probe, baseline_ms, max_candidates, max_frac, kind=De
     Budget: with `patience`, the search stops after that many candidates unless
     the best so far beats baseline_ms by more than min_gain (the caller's memory
     is then already in a fast class, and more candidates would only cost time);
-    with `deadline` (a time.perf_counter() value) no candidate is created after
-    it.  The best candidate found is kept either way."""
+    with `deadline` (a time.perf_counter() value; default SEARCH_BUDGET_S from
+    now) no candidate is created after it.  The best candidate found is kept
+    either way."""
+    if deadline is None:
+        deadline = time.perf_counter() + SEARCH_BUDGET_S
     dev = torch.device(device)
     torch.cuda.empty_cache()  # fresh blocks, not cached free memory
     times = [baseline_ms]
