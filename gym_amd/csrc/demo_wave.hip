@@ -927,25 +927,26 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
     WaveLDS& W = wl[wid];
     DW_PH_DECL;
     const int64_t n64 = (int64_t)nchunks * K;
-    const int64_t total = n64 + (int64_t)ngroups * K;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
-    // The workgroup owns jobs b*8 + w + r*stride (w < 8), i.e. its index i -> job
-    // b*8 + (i & 7) + (i >> 3) * stride, increasing in i: indices [0, nc) are 64x64
-    // chunks, [nc, nt) row groups (the highest job numbers).  Its 8 waves take indices
-    // from one LDS counter, row groups FIRST: a row group costs about two chunks, and
-    // taken last (as a static assignment does) it was the kernel's tail, the wave that
-    // drew it finishing ~0.03 ms after the rest (profiles/r06o_*); taken first, its
-    // siblings take the chunks it would have had.
+    // Job lists per workgroup b: its 64x64 chunks are the static b*8 + w + r*stride
+    // (w < 8: index i -> chunk b*8 + (i & 7) + (i >> 3) * stride, increasing in i), and
+    // its row groups g = b + r*grid (one per workgroup per round, spread over the
+    // workgroups).  Its 8 waves draw from one LDS counter, row groups FIRST: a row group
+    // costs ~2.5 chunks (0.058 ms for the groups alone, profiles/r06p_*), and drawn last
+    // by a static order the ~194 of GPT-2 350M, packed 8 per workgroup into the last
+    // ~25 workgroups, were the kernel's tail; now one workgroup's siblings take the
+    // chunks its group-drawing wave would have had.
     const int64_t b8 = (int64_t)blockIdx.x * kWaves;
-    auto below = [&](int64_t lim) {  // this workgroup's indices whose job is < lim (32-bit:
-        const uint32_t st = (uint32_t)stride;  // the launch keeps the job space below 2^31)
-        uint32_t c = 0;
+    const int64_t g_total = (int64_t)ngroups * K;
+    const uint32_t st = (uint32_t)stride;  // 32-bit counts: the launch keeps the job space below 2^31
+    uint32_t nc32 = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w)
-            if (b8 + w < lim) c += ((uint32_t)(lim - (b8 + w)) + st - 1u) / st;
-        return (int64_t)c;
-    };
-    const int64_t nc = below(n64), nt = below(total), ng = nt - nc;
+    for (int w = 0; w < kWaves; ++w)
+        if (b8 + w < n64) nc32 += ((uint32_t)(n64 - (b8 + w)) + st - 1u) / st;
+    const int64_t nc = nc32;
+    const int64_t ng = (int64_t)blockIdx.x < g_total
+                           ? ((uint32_t)(g_total - blockIdx.x) + gridDim.x - 1u) / gridDim.x : 0;
+    const int64_t nt = nc + ng;
     int tix = -1;
     int64_t last_rep = -1;
     while (true) {
@@ -955,8 +956,8 @@ __global__ __launch_bounds__(kThreads) void encode_kernel(
         if (lane_id() == 0) tv = atomicAdd(&next_job, 1);
         const int64_t t = __builtin_amdgcn_readfirstlane(tv);
         if (t >= nt) break;
-        const int64_t i = t < ng ? nc + t : t - ng;
-        const int64_t job = b8 + (i & 7) + (i >> 3) * stride;
+        const int64_t job = t < ng ? n64 + (int64_t)blockIdx.x + t * gridDim.x  // a row group
+                                   : b8 + ((t - ng) & 7) + ((t - ng) >> 3) * stride;
         if (job < n64) {  // a 64x64 chunk
             const int64_t rep = job / nchunks;
             const int chunk = (int)(job - rep * nchunks);
