@@ -1559,9 +1559,24 @@ static void launch_decode_ms(const ga_demo_tensor* tens, int32_t ntens, int32_t 
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         return (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
     }();
+    // Workgroups: not one persistent workgroup per CU but m workgroups per CU, m chosen
+    // for ~1.75 jobs per wave at S >= 2 and ~5.3 at S = 1: the dispatcher then balances
+    // the CUs (a persistent grid waits for its slowest CU) while each wave still
+    // pipelines a few chunks.  A whole number of workgroups per CU matters as much: the
+    // static job order gives the LAST-dispatched workgroups the fewer jobs, and no
+    // partial last round of workgroups runs alone (5418 workgroups for GPT-2 350M's
+    // 86.7k 8-source jobs ran 0.936 ms, 6144 = 24 per CU 0.838 ms).  GPT-2 350M, one
+    // process (profiles/r06t_ab_demo_decode_grid.txt): 8 sources 0.94-0.97 ms persistent,
+    // 0.838-0.846 ms at 24 per CU, 0.94-0.99 ms at one job per wave; one source
+    // 0.857-0.867 ms persistent, 0.841-0.844 ms at 8 per CU.
     const int64_t jobs = (int64_t)nchunks + ngroups;
     const int64_t want = (jobs + kWaves - 1) / kWaves;
-    const int grid = (int)(want < resident ? want : resident);
+    const int64_t wr = (int64_t)kWaves * resident;  // waves resident at once
+    int64_t m = S >= 2 ? (8 * jobs + 7 * wr) / (14 * wr)    // round(jobs / (1.75 wr))
+                       : (6 * jobs + 16 * wr) / (32 * wr);  // round(jobs / (5.33 wr))
+    if (m < 1) m = 1;
+    const int64_t g = resident * m;
+    const int grid = (int)(g < want ? g : want);
     if (grid <= 0) return;
     if (S >= 2)  // several sources: non-temporal grad stores
         hipLaunchKernelGGL((decode_kernel<T, MS, true>), dim3(grid), dim3(kThreads), 0, stream, tens, ntens, nchunks,
