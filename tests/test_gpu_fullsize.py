@@ -202,6 +202,165 @@ def test_demo_gpt2_350m_sampled_chunks():
     tally.done()
 
 
+def test_demo_gpt2_350m_whole_arena_fp64():
+    """configs[4], ONE node, EVERY chunk of GPT-2 350M (86.7k 64x64 chunks and the
+    1x64 rows): the codec kernels against the oracle's arithmetic in float64,
+    evaluated on the GPU (oracle.demo's DCT-II bases, Y = F1^T X F2 per chunk,
+    top-k by |y| with the lowest index winning ties, the residual X - IDCT(top-k),
+    the decode's sign(IDCT(top-k)) and p - lr * sign; demo.py:159-209, 315-352).
+    Where the k-th magnitude is firm (k-th minus (k+1)-th > 1e-5 of the chunk's
+    largest): the index set exact, the values within 1e-5 of the largest, the
+    residual within 1e-6 of the chunk's largest input; every decided sign exact.
+    At least 99.5% of the chunks must be firm."""
+    from gym_amd import ops
+    from gym_amd.demo_codec import DemoPlan
+    lr, decay = 1e-3, 0.999
+    L, gx = _arena("gpt2-350m", 1, 21)
+    plan = DemoPlan(L, chunk=64, topk=32)
+    assert plan.wave_encode
+    G = gx.mul_(1e-2)
+    X32 = G * torch.tensor(lr, dtype=torch.float32, device=DEV)  # delta = 0: x = RN(lr * g), as the kernel
+    P = torch.randn(1, L.n, device=DEV) * 0.02
+    P0 = P.clone()
+    D = torch.zeros(1, L.n, device=DEV)
+    payload = torch.zeros(1, 2 * plan.M, dtype=torch.int32, device=DEV)
+    ops.demo_encode(plan, P, G, D, payload, lr, decay, 1.0)
+    Gout = torch.zeros(1, L.n, device=DEV)
+    ops.demo_decode(plan, payload, P, Gout, lr)
+    torch.cuda.synchronize()
+    gidx = payload[0, :plan.M]
+    gval = payload[0, plan.M:2 * plan.M].view(torch.float32)
+    f64 = torch.float64
+    bases = {}
+
+    def basis(n):
+        if n not in bases:
+            bases[n] = torch.as_tensor(odemo.dct_basis(n), dtype=f64, device=DEV)
+        return bases[n]
+
+    def chunked(v, R, C, n1, n2):  # [gy * gx, n1, n2]
+        return v.reshape(R // n1, n1, C // n2, n2).permute(0, 2, 1, 3).reshape(-1, n1, n2)
+
+    e0, chunks, firm_chunks = 0, 0, 0
+    dec_firm = dec_total = 0
+    for ti, (shape, off, nel) in enumerate(zip(L.shapes, L.offsets, L.numels)):
+        ne = plan.entries_per_tensor[ti]
+        R, C, n1, n2 = odemo.tensor_view(shape, 64)
+        kk = max(1, min(32, n1 * n2))
+        x = chunked(X32[0, off:off + nel], R, C, n1, n2).to(f64)
+        F1, F2 = basis(n1), basis(n2)
+        Y = torch.einsum("chw,hb,wd->cbd", x, F1, F2).reshape(x.shape[0], n1 * n2)
+        a, order = torch.sort(Y.abs(), dim=1, descending=True, stable=True)
+        scale = a[:, 0]
+        firm = (a[:, kk - 1] - a[:, kk] > 1e-5 * scale) if kk < n1 * n2 else torch.ones_like(scale, dtype=torch.bool)
+        oidx = torch.sort(order[:, :kk], dim=1).values
+        oval = torch.gather(Y, 1, oidx)
+        nch = x.shape[0]
+        gi = gidx[e0:e0 + nch * kk].reshape(nch, kk).long()
+        gv = gval[e0:e0 + nch * kk].reshape(nch, kk).to(f64)
+        bad = firm & (gi != oidx).any(dim=1)
+        assert not bad.any(), (shape, int(bad.sum()), int(bad.nonzero()[0]))
+        dv = ((gv - oval).abs() > 1e-5 * scale[:, None]).any(dim=1) & firm
+        assert not dv.any(), (shape, int(dv.sum()))
+        # the residual delta = x - IDCT(top-k) and the decode of this payload
+        Ym = torch.zeros_like(Y).scatter_(1, oidx, oval).reshape(nch, n1, n2)
+        Rk = torch.einsum("cbd,hb,wd->chw", Ym, F1, F2)  # IDCT: B = F^T
+        dch = chunked(D[0, off:off + nel], R, C, n1, n2).to(f64)
+        xmax = x.abs().reshape(nch, -1).amax(dim=1)
+        dd = ((dch - (x - Rk)).abs().reshape(nch, -1).amax(dim=1) > 1e-6 * xmax) & firm
+        assert not dd.any(), (shape, int(dd.sum()))
+        sg = torch.sign(Rk)
+        decided = (Rk.abs() > 1e-5 * Rk.abs().reshape(nch, -1).amax(dim=1)[:, None, None]) & firm[:, None, None]
+        gs = chunked(Gout[0, off:off + nel], R, C, n1, n2).to(f64)
+        assert not ((gs != sg) & decided).any(), (shape, int(((gs != sg) & decided).sum()))
+        pg = chunked(P[0, off:off + nel], R, C, n1, n2)
+        p0 = chunked(P0[0, off:off + nel], R, C, n1, n2)
+        want_p = p0 - torch.tensor(lr, dtype=torch.float32, device=DEV) * sg.float()
+        assert not (((pg - want_p).abs() > 1e-7) & decided).any(), shape
+        chunks += nch
+        firm_chunks += int(firm.sum())
+        dec_firm += int(decided.sum())
+        dec_total += decided.numel()
+        e0 += ne
+    assert e0 == plan.M and chunks > 86000, (e0, plan.M, chunks)
+    assert firm_chunks >= 0.995 * chunks, (firm_chunks, chunks)
+    assert dec_firm >= 0.95 * dec_total, (dec_firm, dec_total)
+
+
+def test_demo_gpt2_350m_four_nodes_whole_arena_fp64():
+    """configs[4] as four nodes run it, EVERY chunk of GPT-2 350M: each node
+    encodes its OWN gradient, the four payloads are decoded in node order on the
+    shared parameters.  Against float64 on the GPU: each node's index set where
+    its k-th magnitude is firm; the decoded sign -- the gathered entries'
+    scatter-mean (demo.py:331-352) -> IDCT -> sign -- exact wherever decided,
+    with p = p0 - lr * sign there (the sampled oracle test above, whole-arena)."""
+    from gym_amd import ops
+    from gym_amd.demo_codec import DemoPlan
+    lr, decay, S = 1e-3, 0.999, 4
+    L, G = _arena("gpt2-350m", S, 23)
+    plan = DemoPlan(L, chunk=64, topk=32)
+    G.mul_(1e-2)
+    X32 = G * torch.tensor(lr, dtype=torch.float32, device=DEV)
+    P = torch.randn(1, L.n, device=DEV) * 0.02
+    P0 = P.clone()
+    D = torch.zeros(S, L.n, device=DEV)
+    payload = torch.zeros(S, 2 * plan.M, dtype=torch.int32, device=DEV)
+    for k in range(S):
+        ops.demo_encode(plan, P, G[k:k + 1], D[k:k + 1], payload[k:k + 1], lr, decay, 1.0)
+    Gout = torch.zeros(1, L.n, device=DEV)
+    ops.demo_decode(plan, payload, P, Gout, lr)
+    torch.cuda.synchronize()
+    f64 = torch.float64
+    gidx = payload[:, :plan.M].long()
+    gval = payload[:, plan.M:2 * plan.M].contiguous().view(torch.float32).to(f64)
+
+    def chunked(v, R, C, n1, n2):
+        return v.reshape(R // n1, n1, C // n2, n2).permute(0, 2, 1, 3).reshape(-1, n1, n2)
+
+    e0, chunks, firm_sets, sets = 0, 0, 0, 0
+    dec_firm = dec_total = 0
+    for ti, (shape, off, nel) in enumerate(zip(L.shapes, L.offsets, L.numels)):
+        ne = plan.entries_per_tensor[ti]
+        R, C, n1, n2 = odemo.tensor_view(shape, 64)
+        kk = max(1, min(32, n1 * n2))
+        F1 = torch.as_tensor(odemo.dct_basis(n1), dtype=f64, device=DEV)
+        F2 = torch.as_tensor(odemo.dct_basis(n2), dtype=f64, device=DEV)
+        nch = (R // n1) * (C // n2)
+        sums = torch.zeros(nch, n1 * n2, dtype=f64, device=DEV)
+        hits = torch.zeros(nch, n1 * n2, dtype=f64, device=DEV)
+        for k in range(S):  # each node's own top-k set, where it is decided
+            x = chunked(X32[k, off:off + nel], R, C, n1, n2).to(f64)
+            Y = torch.einsum("chw,hb,wd->cbd", x, F1, F2).reshape(nch, n1 * n2)
+            a, order = torch.sort(Y.abs(), dim=1, descending=True, stable=True)
+            firm = (a[:, kk - 1] - a[:, kk] > 1e-5 * a[:, 0]) if kk < n1 * n2 else torch.ones(nch, dtype=torch.bool,
+                                                                                               device=DEV)
+            oidx = torch.sort(order[:, :kk], dim=1).values
+            gi = gidx[k, e0:e0 + nch * kk].reshape(nch, kk)
+            assert not (firm & (gi != oidx).any(dim=1)).any(), (shape, k)
+            firm_sets += int(firm.sum())
+            sets += nch
+            gv = gval[k, e0:e0 + nch * kk].reshape(nch, kk)
+            sums.scatter_add_(1, gi, gv)
+            hits.scatter_add_(1, gi, torch.ones_like(gv))
+        Xm = torch.where(hits > 0, sums / hits.clamp(min=1), torch.zeros_like(sums)).reshape(nch, n1, n2)
+        ghat = torch.einsum("cbd,hb,wd->chw", Xm, F1, F2)
+        decided = ghat.abs() > 1e-5 * ghat.abs().reshape(nch, -1).amax(dim=1).clamp(min=1e-30)[:, None, None]
+        sg = torch.sign(ghat)
+        gs = chunked(Gout[0, off:off + nel], R, C, n1, n2).to(f64)
+        assert not ((gs != sg) & decided).any(), (shape, int(((gs != sg) & decided).sum()))
+        pg = chunked(P[0, off:off + nel], R, C, n1, n2)
+        p0 = chunked(P0[0, off:off + nel], R, C, n1, n2)
+        want_p = p0 - torch.tensor(lr, dtype=torch.float32, device=DEV) * sg.float()
+        assert not (((pg - want_p).abs() > 1e-7) & decided).any(), shape
+        chunks += nch
+        dec_firm += int(decided.sum())
+        dec_total += decided.numel()
+        e0 += ne
+    assert e0 == plan.M and chunks > 86000
+    assert firm_sets >= 0.995 * sets, (firm_sets, sets)
+    assert dec_firm >= 0.95 * dec_total, (dec_firm, dec_total)
+
+
 def _chunks(t2d, R, C, n1, n2, cidx):
     """[len(cidx), n1, n2] chunks (row-major chunk ids) of a [R, C] device view, on the host."""
     gy, gxc = R // n1, C // n2
