@@ -1296,22 +1296,6 @@ __device__ __forceinline__ void dchunk_entries(const ga_demo_tensor& td, int c, 
     }
 }
 
-// the same from a chunk's entry offset e0 and k
-template <int MS>
-__device__ __forceinline__ void dchunk_entries_at(int k, int64_t e0, const int32_t* __restrict__ payload,
-                                                  int64_t pstride, int64_t M, int S, DecIn<MS>& in) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int s = 0; s < MS; ++s) {
-        in.xs[s] = -1;
-        in.vs[s] = 0.f;
-        if (s < S && lane < k) {
-            in.xs[s] = payload[(int64_t)s * pstride + e0 + lane];
-            in.vs[s] = reinterpret_cast<const float*>(payload + (int64_t)s * pstride + M)[e0 + lane];
-        }
-    }
-}
-
 template <typename T>
 __device__ __forceinline__ void dchunk_params(const ga_demo_tensor& td, int c, const T* param, int ptr_vec,
                                               PRaw<T>& p0) {
