@@ -774,6 +774,50 @@ def bench_demo(args, coll, dev, model="gpt2-350m"):
             "placement": placement}
 
 
+def bench_demo_bf16(args, coll, dev, model="gpt2-350m"):
+    """DeMo on bf16 parameters (one node, GPT-2 350M): the default transform
+    (fp32 bases and arithmetic on the bf16 values: the wave kernels) and
+    bf16_transform="reference" (GA_BF16_REF: the reference's bf16 bases and
+    per-stage bf16 rounding, bit-identical to torch's op sequence on the GPU:
+    the block kernels).  Kernel GPU time queued back to back, as the fp32 DeMo
+    line; 1-source and 8-source decodes.  No BASELINE config is bf16: this
+    prices the drop-in's bf16 path."""
+    if coll.world > 1:
+        return {"skipped": "single-GPU kernel timing"}
+    from gym_amd.demo_codec import DemoPlan
+    shapes = MODELS[model]()
+    layout = ArenaLayout(shapes)
+    bf = torch.bfloat16
+    P = synth_replicas(layout, 1, 0, dev).data.to(bf)
+    G = synth_replicas(layout, 1, 7, dev).data.to(bf)
+    D = torch.zeros_like(P)
+    out = {"model": model, "dtype": "bf16"}
+    reps_q = max(args.steps, 10)
+    for name in ("fp32", "reference"):
+        plan = DemoPlan(layout, chunk=64, topk=32, bf16_transform=name).to(dev)
+        pay = torch.zeros(8, 2 * plan.M, dtype=torch.int32, device=dev)
+        gk = torch.Generator(device=dev)
+        Gk = torch.empty_like(G)
+        for k in range(8):  # 8 nodes' own payloads, as the fp32 line's 8-source decode
+            gk.manual_seed(7 + k)
+            Gk.copy_(torch.randn(G.shape, device=dev, generator=gk).mul_(1e-3))
+            D.zero_()
+            ops.demo_encode(plan, P, Gk, D, pay[k:k + 1], 1e-3, 0.999, 1.0)
+        del Gk
+        D.zero_()
+        enc = queued_ms(lambda: ops.demo_encode(plan, P, G, D, pay[0:1], 1e-3, 0.999, 1.0), reps_q, dev)
+        dec1 = queued_ms(lambda: ops.demo_decode(plan, pay[0:1], P, G, 1e-3), reps_q, dev)
+        dec8 = queued_ms(lambda: ops.demo_decode(plan, pay, P, G, 1e-3), reps_q, dev)
+        n = numel(shapes)
+        byt = 6 * n + 8 * plan.M  # bf16: read delta, g; write delta (2 B each) + the payload
+        out[f"transform_{name}"] = {
+            "kernels": "wave (ga_demo_encode_sym / decode_sym)" if plan.wave_encode else "block (ga_demo_encode / decode)",
+            "encode_ms": round(enc, 4), "decode_ms": round(dec1, 4), "decode_8src_ms": round(dec8, 4),
+            "encode_frac_hbm": round(byt / (enc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        del pay
+    return out
+
+
 def bench_diloco_torch_gpu(args, coll, dev, fused_ms, model="gpt2-124m", K=8):
     """The reference's DiLoCo outer step (diloco.py:34-76) as per-tensor torch
     ops on this GPU, the un-fused baseline on the same hardware: for each of
@@ -997,7 +1041,8 @@ def main():
                   ("simple_reduce_char_k8", bench_simple),
                   # the same mean over GPT-2 124M gradients (SimpleReduce / FedAvg in the replica loop)
                   ("simple_reduce_124m_k8", lambda a, c, d: bench_simple(a, c, d, model="gpt2-124m")),
-                  ("demo_350m", bench_demo), ("inner_adamw_clip_124m", bench_inner_adamw)]
+                  ("demo_350m", bench_demo), ("demo_350m_bf16", bench_demo_bf16),
+                  ("inner_adamw_clip_124m", bench_inner_adamw)]
     if args.only and args.only != "diloco":
         fn = {"sparta": bench_sparta, "simple": bench_simple, "demo": bench_demo,
               "adamw": bench_inner_adamw, **dict(extra_runs)}[args.only]
