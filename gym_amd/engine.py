@@ -28,6 +28,14 @@ def _f32(x):
 
 
 CHUNK_BYTES = 64 << 20  # pipeline chunk of the sharded exchange (RCCL stays at its large-message rate)
+# ...and each rank's piece of a chunk (what one reduce-scatter delivers to it,
+# one all-gather takes from it) at least this large, so wide worlds cut the
+# arena into fewer, larger collectives (G=8: 128 MB chunks, 16 MB per rank).
+PIECE_BYTES = 16 << 20
+
+
+def chunk_bytes(world):
+    return max(CHUNK_BYTES, world * PIECE_BYTES)
 # Below this arena size the exchange is latency-bound: ONE all-reduce (RCCL's
 # low-latency protocols, one launch) beats a reduce-scatter + shard kernel +
 # all-gather, and the replicated local update costs microseconds.
@@ -59,7 +67,7 @@ class ShardPlan:
             raise ValueError(f"arena length {n} is not a multiple of world*{align} = {unit}")
         units = n // unit
         if chunks is None:
-            chunks = max(1, -(-n * elem_bytes // CHUNK_BYTES))
+            chunks = max(1, -(-n * elem_bytes // chunk_bytes(world)))
         C = max(1, min(int(chunks), units))
         base, rem = divmod(units, C)
         self.n, self.world, self.rank = n, world, rank

@@ -81,3 +81,22 @@ def test_exchange_sharding_follows_arena_size():
     assert not default_shard(rccl8, SHARD_MIN_BYTES // 4, torch.bfloat16)
     assert not default_shard(SimpleNamespace(rccl=False, exchange=True), 1 << 30, torch.float32)
     assert not default_shard(SimpleNamespace(rccl=True, exchange=False), 1 << 30, torch.float32)
+
+
+def test_exchange_chunks_follow_world():
+    """The sharded exchange's chunks: ~64 MB up to world 4, and each rank's piece
+    at least PIECE_BYTES beyond (GPT-2 124M at world 8: 4 chunks of ~128 MB,
+    ~16 MB per rank); the pieces tile the arena and each rank's shard."""
+    from gym_amd.engine import PIECE_BYTES, ShardPlan
+    from gym_amd.shapes import MODELS, numel
+    n0 = numel(MODELS["gpt2-124m"]())
+    for world, want in [(1, 8), (2, 8), (4, 8), (8, 4)]:
+        n = -(-n0 // (8 * 64)) * 8 * 64
+        plans = [ShardPlan(n, world, r, 4) for r in range(world)]
+        assert len(plans[0].bounds) == want, world
+        assert plans[0].bounds[0][0] == 0 and plans[0].bounds[-1][1] == n
+        for p in plans:
+            assert p.per * world == n
+            assert all(b - a == (c1 - c0) // world for (a, b), (c0, c1) in zip(p.own, p.bounds))
+        if world == 8:
+            assert min(b - a for a, b in plans[0].own) * 4 >= PIECE_BYTES * 0.9
