@@ -431,6 +431,10 @@ __device__ __forceinline__ void chunk64_tail(const f32x16 (&Y)[2][2], int k, T* 
     // ---- top-k: register t = 32 par + 16 qc + r holds coefficient
     //      b = 2 rowmap(r, h) + par, d = 2 l + qc
     const int lane = lane_id(), l = lane & 31, h = lane >> 5;
+    // the top-k's chain of ballot rounds and LDS round trips at raised priority: the
+    // partner wave's products fill its gaps, not the other way round (encode -0.8 to
+    // -1.4% in 12 same-process pairs, profiles/r06ah_ab_demo_encode_topk_priority.txt)
+    __builtin_amdgcn_s_setprio(1);
     auto posof = [&](int par, int qc, int r) -> uint32_t {
         return (uint32_t)((2 * rowmap(r, h) + par) * 64 + 2 * l + qc);
     };
@@ -672,6 +676,7 @@ __device__ __forceinline__ void chunk64_tail(const f32x16 (&Y)[2][2], int k, T* 
         WAVE_LDS_SYNC();
     }
     DW_PH(3);
+    __builtin_amdgcn_s_setprio(0);
     // ---- residual (demo.py:174-180) in the load layout: R^T per parity of b, one
     //      column half H at a time
     uint2* lstp = reinterpret_cast<uint2*>(W.lst);  // [parity][64] entries
